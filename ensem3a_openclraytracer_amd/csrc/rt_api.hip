@@ -1,0 +1,673 @@
+// C-ABI of the MI355X path tracer (include/rt_api.h, include/rt_debug.h).
+//
+// Replaces the pyopencl side of the reference's KernelLauncher
+// (KernelLauncher.py:8-103): device selection, buffer/image uploads, the
+// kernel enqueue and the blocking read-back.  Scene arrays arrive in the
+// reference's flat AoS layouts (FileManager.Scene / BVH.exportArray) and are
+// repacked here into the device layout of rt_internal.h:
+//   * triangles pre-gathered (a.p, e1, e2) + hit record (a.n, material),
+//   * BVH2 nodes holding both child boxes in BFS order (FAST traversal),
+//   * the untouched 9-float export (REF traversal).
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <algorithm>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/rt_api.h"
+#include "../../include/rt_debug.h"
+#include "rt_internal.h"
+
+namespace {
+
+thread_local std::string g_thread_error;
+
+struct DevBuf {
+    void* p = nullptr;
+    size_t bytes = 0;
+};
+
+struct Device {
+    int id = 0;
+    hipStream_t stream = nullptr;
+    DevBuf nodes, bvh9, tri_geo, tri_shade, mat, ibl, out, counts, scratch_a, scratch_b;
+    float* host_stage = nullptr;  // pinned staging for rt_render
+    size_t host_stage_bytes = 0;
+};
+
+// Host copy of the packed scene (kept to upload on every device).
+struct HostScene {
+    std::vector<float> nodes;      // 16 floats per internal node
+    std::vector<float> bvh9;
+    std::vector<float> tri_geo;    // 12 floats per triangle
+    std::vector<float> tri_shade;  // 4 floats per triangle
+    std::vector<float> mat;
+    int32_t nnodes = 0, root_ref = 0, ntri = 0, nmat = 0, nbvh9 = 0, depth = 1;
+    float root_box[6] = {0, 0, 0, 0, 0, 0};
+    bool fast_ok = false;
+};
+
+}  // namespace
+
+struct rt_ctx {
+    std::vector<Device> devs;
+    HostScene hs;
+    bool have_scene = false;
+    bool have_env = false;
+    int ibl_w = 0, ibl_h = 0;
+    int traversal = RT_TRAVERSAL_FAST;
+    int block = 128;
+    std::string err;
+};
+
+namespace {
+
+int set_err(rt_ctx* ctx, int code, const char* fmt, ...) {
+    char buf[1024];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    if (ctx) ctx->err = buf;
+    g_thread_error = buf;
+    return code;
+}
+
+#define HIP_OR_RET(ctx, call)                                                                           \
+    do {                                                                                                \
+        hipError_t e_ = (call);                                                                         \
+        if (e_ != hipSuccess)                                                                           \
+            return set_err((ctx), RT_ERR_HIP, "%s failed: %s", #call, hipGetErrorString(e_));           \
+    } while (0)
+
+hipError_t ensure(DevBuf& b, size_t bytes) {
+    if (b.bytes >= bytes && b.p) return hipSuccess;
+    if (b.p) {
+        hipError_t e = hipFree(b.p);
+        if (e != hipSuccess) return e;
+        b.p = nullptr;
+        b.bytes = 0;
+    }
+    if (bytes == 0) return hipSuccess;
+    hipError_t e = hipMalloc(&b.p, bytes);
+    if (e == hipSuccess) b.bytes = bytes;
+    return e;
+}
+
+void release(DevBuf& b) {
+    if (b.p) (void)hipFree(b.p);
+    b.p = nullptr;
+    b.bytes = 0;
+}
+
+inline int32_t as_i32(float f) {
+    int32_t i;
+    std::memcpy(&i, &f, 4);
+    return i;
+}
+inline float as_f32(int32_t i) {
+    float f;
+    std::memcpy(&f, &i, 4);
+    return f;
+}
+
+// Reference index stored as float -> int, like (int)BVH[...] in MathLib.cl.
+// Returns false for values the kernel could not use safely.
+inline bool fidx(float v, int64_t limit, int32_t* out) {
+    if (!(v == v) || v < -1.0f || v >= (float)limit + 1.0f) return false;
+    const int32_t i = (int32_t)v;
+    if (i < -1 || i >= limit) return false;
+    *out = i;
+    return true;
+}
+
+// Pack the FAST layout from the reference export.  Returns false (with
+// reason) if the export is not a proper binary tree with one triangle per
+// leaf, in which case only the REF traversal is available.
+bool pack_fast(HostScene& hs, const float* bvh9, int64_t nn, int64_t ntri, std::string& why) {
+    std::vector<int32_t> L(nn), R(nn), T(nn);
+    for (int64_t i = 0; i < nn; ++i) {
+        if (!fidx(bvh9[9 * i + 0], nn, &L[i]) || !fidx(bvh9[9 * i + 1], nn, &R[i]) ||
+            !fidx(bvh9[9 * i + 8], ntri, &T[i])) {
+            why = "index out of range";
+            return false;
+        }
+    }
+    // Classify reachable nodes, check the tree shape.
+    std::vector<uint8_t> seen(nn, 0);
+    std::vector<int32_t> wide_of(nn, -1);
+    std::vector<int32_t> bfs;
+    bfs.reserve(nn);
+    auto is_leaf = [&](int64_t i) { return L[i] == -1 && R[i] == -1 && T[i] >= 0; };
+    auto is_inner = [&](int64_t i) { return L[i] >= 0 && R[i] >= 0 && T[i] == -1; };
+    if (!is_leaf(0) && !is_inner(0)) {
+        why = "root is neither a one-triangle leaf nor a two-child node";
+        return false;
+    }
+    std::vector<int32_t> tri_seen(ntri, 0);
+    // BFS over internal nodes
+    seen[0] = 1;
+    if (is_inner(0)) {
+        bfs.push_back(0);
+        wide_of[0] = 0;
+    }
+    std::vector<int32_t> depth_of(nn, 0);
+    int32_t max_depth = 1;
+    for (size_t h = 0; h < bfs.size(); ++h) {
+        const int32_t n = bfs[h];
+        for (int32_t ch : {L[n], R[n]}) {
+            if (seen[ch]) {
+                why = "node reachable twice (not a tree)";
+                return false;
+            }
+            seen[ch] = 1;
+            if (is_inner(ch)) {
+                wide_of[ch] = (int32_t)bfs.size();
+                depth_of[ch] = depth_of[n] + 1;
+                if (depth_of[ch] + 1 > max_depth) max_depth = depth_of[ch] + 1;
+                bfs.push_back(ch);
+            } else if (is_leaf(ch)) {
+                if (tri_seen[T[ch]]++) {
+                    why = "triangle in two leaves";
+                    return false;
+                }
+            } else {
+                why = "node with one child, or with both a triangle and children";
+                return false;
+            }
+        }
+    }
+    if (is_leaf(0)) tri_seen[T[0]]++;
+    // Rank of each leaf triangle in the reference visiting order: pre-order
+    // DFS, right child first (push left then right, MathLib.cl:269-276).
+    std::vector<int32_t> rank(ntri, 0x7fffffff);
+    {
+        std::vector<int32_t> st;
+        st.push_back(0);
+        int32_t r = 0;
+        while (!st.empty()) {
+            const int32_t n = st.back();
+            st.pop_back();
+            if (T[n] >= 0) rank[T[n]] = r++;
+            if (L[n] >= 0) st.push_back(L[n]);
+            if (R[n] >= 0) st.push_back(R[n]);
+        }
+    }
+    hs.nnodes = (int32_t)bfs.size();
+    hs.nodes.assign((size_t)hs.nnodes * 16, 0.0f);
+    for (size_t w = 0; w < bfs.size(); ++w) {
+        const int32_t n = bfs[w];
+        const float* c0 = bvh9 + 9 * (int64_t)L[n];
+        const float* c1 = bvh9 + 9 * (int64_t)R[n];
+        float* o = hs.nodes.data() + 16 * w;
+        o[0] = c0[2]; o[1] = c0[5]; o[2] = c0[3]; o[3] = c0[6];
+        o[4] = c1[2]; o[5] = c1[5]; o[6] = c1[3]; o[7] = c1[6];
+        o[8] = c0[4]; o[9] = c0[7]; o[10] = c1[4]; o[11] = c1[7];
+        const int32_t r0 = is_inner(L[n]) ? wide_of[L[n]] : ~T[L[n]];
+        const int32_t r1 = is_inner(R[n]) ? wide_of[R[n]] : ~T[R[n]];
+        o[12] = as_f32(r0); o[13] = as_f32(r1); o[14] = 0.0f; o[15] = 0.0f;
+    }
+    hs.root_ref = is_inner(0) ? 0 : ~T[0];
+    for (int k = 0; k < 3; ++k) { hs.root_box[k] = bvh9[2 + k]; hs.root_box[3 + k] = bvh9[5 + k]; }
+    hs.depth = max_depth;
+    for (int64_t t = 0; t < ntri; ++t) hs.tri_geo[12 * t + 3] = as_f32(rank[t]);
+    return true;
+}
+
+template <typename T>
+hipError_t upload(DevBuf& b, const std::vector<T>& v, hipStream_t s) {
+    const size_t bytes = v.size() * sizeof(T);
+    hipError_t e = ensure(b, bytes > 0 ? bytes : 16);
+    if (e != hipSuccess || bytes == 0) return e;
+    return hipMemcpyAsync(b.p, v.data(), bytes, hipMemcpyHostToDevice, s);
+}
+
+rt::DevScene dev_scene(const rt_ctx* ctx, const Device& d) {
+    rt::DevScene s{};
+    s.nodes = (const float4*)d.nodes.p;
+    s.nnodes = ctx->hs.nnodes;
+    s.root_ref = ctx->hs.root_ref;
+    for (int k = 0; k < 6; ++k) s.root_box[k] = ctx->hs.root_box[k];
+    s.bvh9 = (const float*)d.bvh9.p;
+    s.nbvh9 = ctx->hs.nbvh9;
+    s.tri_geo = (const float4*)d.tri_geo.p;
+    s.tri_shade = (const float4*)d.tri_shade.p;
+    s.ntri = ctx->hs.ntri;
+    s.mat = (const float*)d.mat.p;
+    s.nmat = ctx->hs.nmat;
+    s.ibl = (const uchar4*)d.ibl.p;
+    s.ibl_w = ctx->ibl_w;
+    s.ibl_h = ctx->ibl_h;
+    s.depth = ctx->hs.depth;
+    return s;
+}
+
+int check_frame(rt_ctx* ctx, const float* cam, const float* env, int64_t npix, int spp, int row0, int row_step,
+                rt::FrameParams* fp) {
+    if (!ctx) return set_err(nullptr, RT_ERR_ARG, "null context");
+    if (!ctx->have_scene) return set_err(ctx, RT_ERR_STATE, "rt_set_scene has not been called");
+    if (!ctx->have_env) return set_err(ctx, RT_ERR_STATE, "rt_set_env has not been called");
+    if (!cam || !env) return set_err(ctx, RT_ERR_ARG, "cam/env must not be NULL");
+    if (!(cam[6] >= 1.0f) || !(cam[6] < 2147483648.0f))
+        return set_err(ctx, RT_ERR_ARG, "cam[6] (row width) must be >= 1, got %g", (double)cam[6]);
+    if (npix <= 0 || npix > 0x7fffffff) return set_err(ctx, RT_ERR_ARG, "pixel count %lld out of range", (long long)npix);
+    if (spp < 0) return set_err(ctx, RT_ERR_ARG, "spp must be >= 0");
+    if (row0 < 0 || row_step <= 0) return set_err(ctx, RT_ERR_ARG, "bad row tiling (%d, %d)", row0, row_step);
+    std::memcpy(fp->cam, cam, sizeof fp->cam);
+    std::memcpy(fp->env, env, sizeof fp->env);
+    fp->width = (int32_t)cam[6];
+    fp->npix = npix;
+    fp->spp = spp;
+    fp->row0 = row0;
+    fp->row_step = row_step;
+    fp->nloc = rt_tile_rows(npix, fp->width, row0, row_step) * fp->width;
+    fp->log_pixel = -1;
+    fp->log_buf = nullptr;
+    fp->log_cap = 0;
+    fp->log_count = nullptr;
+    return RT_OK;
+}
+
+int effective_traversal(const rt_ctx* ctx) {
+    return (ctx->traversal == RT_TRAVERSAL_FAST && ctx->hs.fast_ok) ? RT_TRAVERSAL_FAST : RT_TRAVERSAL_REF;
+}
+
+}  // namespace
+
+extern "C" {
+
+int rt_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+int rt_create(int n_devices, const int* device_ids, rt_ctx** out) {
+    if (!out) return set_err(nullptr, RT_ERR_ARG, "out must not be NULL");
+    *out = nullptr;
+    int avail = 0;
+    hipError_t e = hipGetDeviceCount(&avail);
+    if (e != hipSuccess || avail <= 0)
+        return set_err(nullptr, RT_ERR_HIP, "no HIP device available (%s)", hipGetErrorString(e));
+    if (n_devices <= 0) n_devices = 1;
+    if (n_devices > avail)
+        return set_err(nullptr, RT_ERR_ARG, "requested %d devices, %d available", n_devices, avail);
+    rt_ctx* ctx = new rt_ctx();
+    ctx->devs.resize(n_devices);
+    for (int i = 0; i < n_devices; ++i) {
+        const int id = device_ids ? device_ids[i] : i;
+        if (id < 0 || id >= avail) {
+            delete ctx;
+            return set_err(nullptr, RT_ERR_ARG, "device id %d out of range", id);
+        }
+        ctx->devs[i].id = id;
+        if ((e = hipSetDevice(id)) != hipSuccess || (e = hipStreamCreateWithFlags(&ctx->devs[i].stream,
+                                                                                 hipStreamNonBlocking)) != hipSuccess) {
+            rt_destroy(ctx);
+            return set_err(nullptr, RT_ERR_HIP, "device %d init failed: %s", id, hipGetErrorString(e));
+        }
+    }
+    *out = ctx;
+    return RT_OK;
+}
+
+void rt_destroy(rt_ctx* ctx) {
+    if (!ctx) return;
+    for (auto& d : ctx->devs) {
+        if (hipSetDevice(d.id) != hipSuccess) continue;
+        if (d.stream) (void)hipStreamSynchronize(d.stream);
+        for (DevBuf* b : {&d.nodes, &d.bvh9, &d.tri_geo, &d.tri_shade, &d.mat, &d.ibl, &d.out, &d.counts,
+                          &d.scratch_a, &d.scratch_b})
+            release(*b);
+        if (d.host_stage) (void)hipHostFree(d.host_stage);
+        if (d.stream) (void)hipStreamDestroy(d.stream);
+    }
+    delete ctx;
+}
+
+const char* rt_last_error(rt_ctx* ctx) { return ctx ? ctx->err.c_str() : g_thread_error.c_str(); }
+
+int rt_set_option(rt_ctx* ctx, const char* key, int64_t value) {
+    if (!ctx || !key) return set_err(ctx, RT_ERR_ARG, "null argument");
+    if (!std::strcmp(key, "traversal")) {
+        if (value != RT_TRAVERSAL_FAST && value != RT_TRAVERSAL_REF)
+            return set_err(ctx, RT_ERR_ARG, "traversal must be 0 (fast) or 1 (ref)");
+        ctx->traversal = (int)value;
+        return RT_OK;
+    }
+    if (!std::strcmp(key, "block")) {
+        if (value != 64 && value != 128 && value != 256) return set_err(ctx, RT_ERR_ARG, "block must be 64/128/256");
+        ctx->block = (int)value;
+        return RT_OK;
+    }
+    return set_err(ctx, RT_ERR_ARG, "unknown option '%s'", key);
+}
+
+int rt_set_scene(rt_ctx* ctx, const float* vp, int64_t nvp, const float* vn, int64_t nvn, const float* vuv,
+                 int64_t nvuv, const int32_t* face, int64_t nface, const float* mat, int64_t nmat, const float* bvh9,
+                 int64_t nbvh) {
+    (void)vuv;
+    (void)nvuv;  // uv is carried by hitInfo but never consumed by the reference kernel
+    if (!ctx) return set_err(nullptr, RT_ERR_ARG, "null context");
+    if (nvp < 0 || nvp % 3 || nvn < 0 || nvn % 3 || nface < 0 || nface % 10 || nmat <= 0 || nmat % 6 || nbvh < 0 ||
+        nbvh % 9)
+        return set_err(ctx, RT_ERR_ARG,
+                       "bad array sizes (V_p %lld, V_n %lld, faceData %lld, materialData %lld, BVH %lld)",
+                       (long long)nvp, (long long)nvn, (long long)nface, (long long)nmat, (long long)nbvh);
+    if ((nface && (!vp || !vn || !face)) || !mat || (nbvh && !bvh9))
+        return set_err(ctx, RT_ERR_ARG, "null array");
+    const int64_t T = nface / 10, NV = nvp / 3, NN = nvn / 3, M = nmat / 6, NB = nbvh / 9;
+    if (T > 0x3fffffff || NB > 0x7fffffff) return set_err(ctx, RT_ERR_ARG, "scene too large");
+    if (T > 0 && NB == 0) return set_err(ctx, RT_ERR_SCENE, "triangles given without a BVH");
+    for (int64_t m = 0; m < M; ++m) {
+        const float tf = mat[6 * m];
+        if (!(tf > -1.0f && tf < 4.0f))
+            return set_err(ctx, RT_ERR_SCENE, "material %lld has type %g; the kernel defines types 0..3", (long long)m,
+                           (double)tf);
+    }
+    HostScene hs;
+    hs.ntri = (int32_t)T;
+    hs.nmat = (int32_t)M;
+    hs.nbvh9 = (int32_t)NB;
+    hs.mat.assign(mat, mat + nmat);
+    if (bvh9) hs.bvh9.assign(bvh9, bvh9 + nbvh);
+    hs.tri_geo.assign((size_t)T * 12, 0.0f);
+    hs.tri_shade.assign((size_t)T * 4, 0.0f);
+    for (int64_t t = 0; t < T; ++t) {
+        const int32_t* f = face + 10 * t;
+        if (f[0] < 0 || f[0] >= M)
+            return set_err(ctx, RT_ERR_ARG, "triangle %lld: material %d out of range [0,%lld)", (long long)t, f[0],
+                           (long long)M);
+        for (int j = 7; j < 10; ++j)
+            if (f[j] < 0 || f[j] >= NV)
+                return set_err(ctx, RT_ERR_ARG, "triangle %lld: position index %d out of range", (long long)t, f[j]);
+        if (f[4] < 0 || f[4] >= NN)
+            return set_err(ctx, RT_ERR_ARG, "triangle %lld: normal index %d out of range", (long long)t, f[4]);
+        const float* a = vp + 3 * (int64_t)f[7];
+        const float* b = vp + 3 * (int64_t)f[8];
+        const float* c = vp + 3 * (int64_t)f[9];
+        float* g = hs.tri_geo.data() + 12 * t;
+        g[0] = a[0]; g[1] = a[1]; g[2] = a[2]; g[3] = 0.0f;
+        g[4] = b[0] - a[0]; g[5] = b[1] - a[1]; g[6] = b[2] - a[2]; g[7] = 0.0f;
+        g[8] = c[0] - a[0]; g[9] = c[1] - a[1]; g[10] = c[2] - a[2]; g[11] = 0.0f;
+        const float* n = vn + 3 * (int64_t)f[4];
+        float* sh = hs.tri_shade.data() + 4 * t;
+        sh[0] = n[0]; sh[1] = n[1]; sh[2] = n[2]; sh[3] = as_f32(f[0]);
+    }
+    // REF traversal safety: every index the reference would follow must be in range.
+    for (int64_t i = 0; i < NB; ++i) {
+        int32_t l, r, t;
+        if (!fidx(bvh9[9 * i + 0], NB, &l) || !fidx(bvh9[9 * i + 1], NB, &r) || !fidx(bvh9[9 * i + 8], T, &t))
+            return set_err(ctx, RT_ERR_SCENE, "BVH node %lld has an index out of range", (long long)i);
+    }
+    // The reference loops forever on a cyclic node graph; refuse it instead of hanging the GPU.
+    if (NB > 0) {
+        std::vector<uint8_t> color(NB, 0);  // 0 new, 1 on path, 2 done
+        std::vector<std::pair<int32_t, int>> st;
+        st.push_back({0, 0});
+        color[0] = 1;
+        while (!st.empty()) {
+            auto& top = st.back();
+            const int32_t n = top.first;
+            if (top.second < 2) {
+                const int32_t ch = (int32_t)bvh9[9 * (int64_t)n + top.second];
+                ++top.second;
+                if (ch < 0) continue;
+                if (color[ch] == 1) return set_err(ctx, RT_ERR_SCENE, "BVH node graph has a cycle through node %d", ch);
+                if (color[ch] == 0) { color[ch] = 1; st.push_back({ch, 0}); }
+            } else {
+                color[n] = 2;
+                st.pop_back();
+            }
+        }
+    }
+    std::string why;
+    hs.fast_ok = (T > 0) ? pack_fast(hs, bvh9, NB, T, why) : true;
+    if (T == 0) { hs.nnodes = 0; hs.root_ref = 0; hs.depth = 1; }
+    if (hs.fast_ok && (int64_t)hs.depth * 256 * 4 > 64 * 1024) {
+        hs.fast_ok = false;
+        why = "tree too deep for the LDS stack";
+    }
+    if (hs.nodes.empty()) hs.nodes.assign(16, 0.0f);
+    for (auto& d : ctx->devs) {
+        HIP_OR_RET(ctx, hipSetDevice(d.id));
+        HIP_OR_RET(ctx, upload(d.nodes, hs.nodes, d.stream));
+        HIP_OR_RET(ctx, upload(d.bvh9, hs.bvh9, d.stream));
+        HIP_OR_RET(ctx, upload(d.tri_geo, hs.tri_geo, d.stream));
+        HIP_OR_RET(ctx, upload(d.tri_shade, hs.tri_shade, d.stream));
+        HIP_OR_RET(ctx, upload(d.mat, hs.mat, d.stream));
+        HIP_OR_RET(ctx, hipStreamSynchronize(d.stream));
+    }
+    ctx->hs = std::move(hs);
+    ctx->have_scene = true;
+    if (!ctx->hs.fast_ok) ctx->err = "FAST traversal unavailable (" + why + "); REF traversal will be used";
+    return RT_OK;
+}
+
+int rt_set_env(rt_ctx* ctx, const uint8_t* rgba, int w, int h) {
+    if (!ctx) return set_err(nullptr, RT_ERR_ARG, "null context");
+    if (!rgba || w <= 0 || h <= 0) return set_err(ctx, RT_ERR_ARG, "bad IBL image (%d x %d)", w, h);
+    const size_t bytes = (size_t)w * h * 4;
+    for (auto& d : ctx->devs) {
+        HIP_OR_RET(ctx, hipSetDevice(d.id));
+        HIP_OR_RET(ctx, ensure(d.ibl, bytes));
+        HIP_OR_RET(ctx, hipMemcpyAsync(d.ibl.p, rgba, bytes, hipMemcpyHostToDevice, d.stream));
+        HIP_OR_RET(ctx, hipStreamSynchronize(d.stream));
+    }
+    ctx->ibl_w = w;
+    ctx->ibl_h = h;
+    ctx->have_env = true;
+    return RT_OK;
+}
+
+int64_t rt_tile_rows(int64_t npix, int width, int row0, int row_step) {
+    if (npix <= 0 || width <= 0 || row0 < 0 || row_step <= 0) return 0;
+    const int64_t H = (npix + width - 1) / width;
+    if (row0 >= H) return 0;
+    return (H - row0 + row_step - 1) / row_step;
+}
+
+int rt_render_device(rt_ctx* ctx, int device_index, const float cam[10], const float env[5], int64_t npix, int spp,
+                     int max_bounce, int row0, int row_step, float* d_out, void* stream) {
+    rt::FrameParams fp;
+    int st = check_frame(ctx, cam, env, npix, spp, row0, row_step, &fp);
+    if (st) return st;
+    if (device_index < 0 || device_index >= (int)ctx->devs.size())
+        return set_err(ctx, RT_ERR_ARG, "device index %d out of range", device_index);
+    if (!d_out && fp.nloc > 0) return set_err(ctx, RT_ERR_ARG, "d_out must not be NULL");
+    if (max_bounce > 4096) return set_err(ctx, RT_ERR_ARG, "maxBounce %d > 4096", max_bounce);
+    fp.max_bounce = max_bounce;
+    Device& d = ctx->devs[device_index];
+    HIP_OR_RET(ctx, hipSetDevice(d.id));
+    hipStream_t s = stream ? (hipStream_t)stream : d.stream;
+    HIP_OR_RET(ctx, rt::launch_render(dev_scene(ctx, d), fp, effective_traversal(ctx), ctx->block, d_out, nullptr, s));
+    return RT_OK;
+}
+
+int rt_render(rt_ctx* ctx, const float cam[10], const float env[5], int64_t npix, int spp, int max_bounce,
+              float* out_rgb) {
+    rt::FrameParams fp0;
+    int st = check_frame(ctx, cam, env, npix, spp, 0, 1, &fp0);
+    if (st) return st;
+    if (!out_rgb) return set_err(ctx, RT_ERR_ARG, "out_rgb must not be NULL");
+    if (max_bounce > 4096) return set_err(ctx, RT_ERR_ARG, "maxBounce %d > 4096", max_bounce);
+    const int nd = (int)ctx->devs.size();
+    const int W = fp0.width;
+    // Launch every device, then read back: devices run concurrently.
+    for (int k = 0; k < nd; ++k) {
+        Device& d = ctx->devs[k];
+        rt::FrameParams fp = fp0;
+        fp.row0 = k;
+        fp.row_step = nd;
+        fp.max_bounce = max_bounce;
+        fp.nloc = rt_tile_rows(npix, W, k, nd) * W;
+        HIP_OR_RET(ctx, hipSetDevice(d.id));
+        const size_t bytes = (size_t)fp.nloc * 3 * sizeof(float);
+        if (bytes == 0) continue;
+        HIP_OR_RET(ctx, ensure(d.out, bytes));
+        if (d.host_stage_bytes < bytes) {
+            if (d.host_stage) HIP_OR_RET(ctx, hipHostFree(d.host_stage));
+            d.host_stage = nullptr;
+            d.host_stage_bytes = 0;
+            HIP_OR_RET(ctx, hipHostMalloc((void**)&d.host_stage, bytes, hipHostMallocDefault));
+            d.host_stage_bytes = bytes;
+        }
+        HIP_OR_RET(ctx, rt::launch_render(dev_scene(ctx, d), fp, effective_traversal(ctx), ctx->block,
+                                          (float*)d.out.p, nullptr, d.stream));
+        HIP_OR_RET(ctx, hipMemcpyAsync(d.host_stage, d.out.p, bytes, hipMemcpyDeviceToHost, d.stream));
+    }
+    for (int k = 0; k < nd; ++k) {
+        Device& d = ctx->devs[k];
+        HIP_OR_RET(ctx, hipSetDevice(d.id));
+        HIP_OR_RET(ctx, hipStreamSynchronize(d.stream));
+        const int64_t rows = rt_tile_rows(npix, W, k, nd);
+        if (nd == 1) {
+            std::memcpy(out_rgb, d.host_stage, (size_t)npix * 3 * sizeof(float));
+            continue;
+        }
+        for (int64_t r = 0; r < rows; ++r) {
+            const int64_t gr = (int64_t)k + r * nd;
+            const int64_t first = gr * W;
+            const int64_t count = std::min<int64_t>(W, npix - first);
+            std::memcpy(out_rgb + 3 * first, d.host_stage + 3 * r * W, (size_t)count * 3 * sizeof(float));
+        }
+    }
+    return RT_OK;
+}
+
+int rt_count_work(rt_ctx* ctx, const float cam[10], const float env[5], int64_t npix, int spp, int max_bounce,
+                  int row0, int row_step, uint64_t counts[5]) {
+    rt::FrameParams fp;
+    int st = check_frame(ctx, cam, env, npix, spp, row0, row_step, &fp);
+    if (st) return st;
+    if (!counts) return set_err(ctx, RT_ERR_ARG, "counts must not be NULL");
+    if (max_bounce > 4096) return set_err(ctx, RT_ERR_ARG, "maxBounce %d > 4096", max_bounce);
+    fp.max_bounce = max_bounce;
+    Device& d = ctx->devs[0];
+    HIP_OR_RET(ctx, hipSetDevice(d.id));
+    const size_t bytes = (size_t)fp.nloc * 3 * sizeof(float);
+    HIP_OR_RET(ctx, ensure(d.out, bytes > 0 ? bytes : 16));
+    HIP_OR_RET(ctx, ensure(d.counts, 5 * sizeof(unsigned long long)));
+    HIP_OR_RET(ctx, hipMemsetAsync(d.counts.p, 0, 5 * sizeof(unsigned long long), d.stream));
+    HIP_OR_RET(ctx, rt::launch_render(dev_scene(ctx, d), fp, effective_traversal(ctx), ctx->block, (float*)d.out.p,
+                                      (unsigned long long*)d.counts.p, d.stream));
+    unsigned long long h[5];
+    HIP_OR_RET(ctx, hipMemcpyAsync(h, d.counts.p, sizeof h, hipMemcpyDeviceToHost, d.stream));
+    HIP_OR_RET(ctx, hipStreamSynchronize(d.stream));
+    for (int q = 0; q < 5; ++q) counts[q] = h[q];
+    return RT_OK;
+}
+
+int rt_work_bytes(rt_ctx* ctx, double out[4]) {
+    if (!ctx || !out) return set_err(ctx, RT_ERR_ARG, "null argument");
+    if (effective_traversal(ctx) == RT_TRAVERSAL_FAST) {
+        out[0] = 64.0;  // one BVH2 node: both child boxes + child refs (4 x float4)
+    } else {
+        out[0] = 36.0;  // one reference AoS node (9 floats)
+    }
+    out[1] = 48.0;  // one triangle test: a.p, e1, e2 (+ rank), 3 x float4
+    out[2] = 40.0;  // hit record: normal+material (16 B) + material row (24 B)
+    out[3] = 16.0;  // IBL lookup: 4 RGBA8 texels
+    return RT_OK;
+}
+
+int rt_gamma(rt_ctx* ctx, const float* in, float* out, int64_t n) {
+    if (!ctx) return set_err(nullptr, RT_ERR_ARG, "null context");
+    if (n < 0 || (n > 0 && (!in || !out))) return set_err(ctx, RT_ERR_ARG, "bad arguments");
+    if (n == 0) return RT_OK;
+    Device& d = ctx->devs[0];
+    HIP_OR_RET(ctx, hipSetDevice(d.id));
+    const size_t bytes = (size_t)n * sizeof(float);
+    HIP_OR_RET(ctx, ensure(d.scratch_a, bytes));
+    HIP_OR_RET(ctx, ensure(d.scratch_b, bytes));
+    HIP_OR_RET(ctx, hipMemcpyAsync(d.scratch_a.p, in, bytes, hipMemcpyHostToDevice, d.stream));
+    HIP_OR_RET(ctx, rt::launch_gamma((const float*)d.scratch_a.p, (float*)d.scratch_b.p, n, d.stream));
+    HIP_OR_RET(ctx, hipMemcpyAsync(out, d.scratch_b.p, bytes, hipMemcpyDeviceToHost, d.stream));
+    HIP_OR_RET(ctx, hipStreamSynchronize(d.stream));
+    return RT_OK;
+}
+
+int rt_debug_math(rt_ctx* ctx, int fn, const float* x, const float* y, float* out, int64_t n) {
+    if (!ctx || !x || !out || n < 0) return set_err(ctx, RT_ERR_ARG, "bad arguments");
+    Device& d = ctx->devs[0];
+    HIP_OR_RET(ctx, hipSetDevice(d.id));
+    const size_t bytes = (size_t)n * sizeof(float);
+    if (!bytes) return RT_OK;
+    HIP_OR_RET(ctx, ensure(d.scratch_a, 3 * bytes));
+    float* dx = (float*)d.scratch_a.p;
+    float* dy = dx + n;
+    float* dout = dy + n;
+    HIP_OR_RET(ctx, hipMemcpyAsync(dx, x, bytes, hipMemcpyHostToDevice, d.stream));
+    if (y) HIP_OR_RET(ctx, hipMemcpyAsync(dy, y, bytes, hipMemcpyHostToDevice, d.stream));
+    else HIP_OR_RET(ctx, hipMemsetAsync(dy, 0, bytes, d.stream));
+    HIP_OR_RET(ctx, rt::launch_debug_math(fn, dx, dy, dout, n, d.stream));
+    HIP_OR_RET(ctx, hipMemcpyAsync(out, dout, bytes, hipMemcpyDeviceToHost, d.stream));
+    HIP_OR_RET(ctx, hipStreamSynchronize(d.stream));
+    return RT_OK;
+}
+
+int rt_debug_trace(rt_ctx* ctx, int traversal, const float* rays, float* out, int64_t n) {
+    if (!ctx || !rays || !out || n < 0) return set_err(ctx, RT_ERR_ARG, "bad arguments");
+    if (!ctx->have_scene) return set_err(ctx, RT_ERR_STATE, "no scene");
+    if (traversal == RT_TRAVERSAL_FAST && !ctx->hs.fast_ok)
+        return set_err(ctx, RT_ERR_STATE, "FAST traversal unavailable for this scene");
+    if (!n) return RT_OK;
+    Device& d = ctx->devs[0];
+    HIP_OR_RET(ctx, hipSetDevice(d.id));
+    HIP_OR_RET(ctx, ensure(d.scratch_a, (size_t)n * 6 * sizeof(float)));
+    HIP_OR_RET(ctx, ensure(d.scratch_b, (size_t)n * 2 * sizeof(float)));
+    HIP_OR_RET(ctx, hipMemcpyAsync(d.scratch_a.p, rays, (size_t)n * 6 * sizeof(float), hipMemcpyHostToDevice, d.stream));
+    HIP_OR_RET(ctx, rt::launch_debug_trace(dev_scene(ctx, d), traversal, (const float*)d.scratch_a.p,
+                                           (float*)d.scratch_b.p, n, d.stream));
+    HIP_OR_RET(ctx, hipMemcpyAsync(out, d.scratch_b.p, (size_t)n * 2 * sizeof(float), hipMemcpyDeviceToHost, d.stream));
+    HIP_OR_RET(ctx, hipStreamSynchronize(d.stream));
+    return RT_OK;
+}
+
+int rt_debug_pixel_log(rt_ctx* ctx, int traversal, const float cam[10], const float env[5], int64_t npix, int spp,
+                       int max_bounce, int64_t pixel, float* log, int cap, int* n_events, float out3[3]) {
+    rt::FrameParams fp;
+    if (!cam) return set_err(ctx, RT_ERR_ARG, "null cam");
+    const int W = (int)cam[6];
+    if (W <= 0 || pixel < 0 || pixel >= npix) return set_err(ctx, RT_ERR_ARG, "pixel out of range");
+    int st = check_frame(ctx, cam, env, npix, spp, (int)(pixel / W), (int)npix, &fp);
+    if (st) return st;
+    if (!log || cap <= 0 || !n_events || !out3) return set_err(ctx, RT_ERR_ARG, "bad log buffer");
+    if (traversal == RT_TRAVERSAL_FAST && !ctx->hs.fast_ok) traversal = RT_TRAVERSAL_REF;
+    fp.max_bounce = max_bounce;
+    Device& d = ctx->devs[0];
+    HIP_OR_RET(ctx, hipSetDevice(d.id));
+    const size_t obytes = (size_t)fp.nloc * 3 * sizeof(float);
+    const size_t lbytes = (size_t)cap * 16 * sizeof(float);
+    HIP_OR_RET(ctx, ensure(d.scratch_a, obytes + lbytes + 16));
+    float* dout = (float*)d.scratch_a.p;
+    fp.log_buf = dout + fp.nloc * 3;
+    fp.log_count = (int32_t*)(fp.log_buf + (size_t)cap * 16);
+    fp.log_cap = cap;
+    fp.log_pixel = pixel;
+    HIP_OR_RET(ctx, hipMemsetAsync(fp.log_count, 0, sizeof(int32_t), d.stream));
+    HIP_OR_RET(ctx, rt::launch_debug_log(dev_scene(ctx, d), fp, traversal, dout, d.stream));
+    int32_t n = 0;
+    HIP_OR_RET(ctx, hipMemcpyAsync(&n, fp.log_count, sizeof n, hipMemcpyDeviceToHost, d.stream));
+    HIP_OR_RET(ctx, hipStreamSynchronize(d.stream));
+    if (n > cap) n = cap;
+    HIP_OR_RET(ctx, hipMemcpy(log, fp.log_buf, (size_t)n * 16 * sizeof(float), hipMemcpyDeviceToHost));
+    HIP_OR_RET(ctx, hipMemcpy(out3, dout + 3 * (pixel % W), 3 * sizeof(float), hipMemcpyDeviceToHost));
+    *n_events = n;
+    return RT_OK;
+}
+
+int rt_debug_scene_info(rt_ctx* ctx, int64_t out[4]) {
+    if (!ctx || !out) return set_err(ctx, RT_ERR_ARG, "bad arguments");
+    out[0] = ctx->hs.fast_ok ? 1 : 0;
+    out[1] = ctx->hs.depth;
+    out[2] = ctx->hs.nnodes;
+    out[3] = ctx->hs.ntri;
+    return RT_OK;
+}
+
+}  // extern "C"

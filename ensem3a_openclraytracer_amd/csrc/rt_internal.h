@@ -1,0 +1,64 @@
+// Internal interface between the C-ABI layer (rt_api.hip) and the kernels
+// (rt_kernels.hip).  Not part of the public boundary.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstdint>
+
+namespace rt {
+
+// Device view of one uploaded scene (all pointers are device pointers).
+struct DevScene {
+    // FAST traversal: BVH2 nodes holding both child boxes, 4 x float4 each:
+    //   [0] = c0.min.x, c0.max.x, c0.min.y, c0.max.y
+    //   [1] = c1.min.x, c1.max.x, c1.min.y, c1.max.y
+    //   [2] = c0.min.z, c0.max.z, c1.min.z, c1.max.z
+    //   [3] = child refs (int bits): >= 0 internal node, < 0 leaf = ~triangle
+    const float4* nodes;
+    int32_t nnodes;        // internal nodes in `nodes`
+    int32_t root_ref;      // ref of the root (~tri when the root is a leaf)
+    float root_box[6];     // min.xyz, max.xyz of the root
+    // REF traversal: the reference's own AoS export, 9 floats per node
+    const float* bvh9;
+    int32_t nbvh9;
+    // triangles in reference order: 3 x float4 (a.p | rank, e1 | 0, e2 | 0)
+    const float4* tri_geo;
+    // hit record per triangle: first-vertex normal | material index bits
+    const float4* tri_shade;
+    int32_t ntri;
+    // materials: 6 floats each [type, r, g, b, roughness, ior]
+    const float* mat;
+    int32_t nmat;
+    // IBL RGBA8
+    const uchar4* ibl;
+    int32_t ibl_w, ibl_h;
+    int32_t depth;         // max number of FAST stack entries a ray can need
+};
+
+struct FrameParams {
+    float cam[10];
+    float env[5];
+    int32_t width;       // (int)cam[6]
+    int64_t npix;        // frame pixel count (reference imgSize)
+    int32_t spp;
+    int32_t max_bounce;
+    int32_t row0, row_step;
+    int64_t nloc;        // pixels in this tile = rows * width
+    // debug event log of one pixel (rt_debug_pixel_log only; unused by the product launches)
+    int64_t log_pixel;
+    float* log_buf;
+    int32_t log_cap;
+    int32_t* log_count;
+};
+
+// Launch the render kernel; counts != nullptr selects the instrumented build
+// (device pointer to 5 uint64 accumulators).
+hipError_t launch_render(const DevScene& sc, const FrameParams& fp, int traversal, int block,
+                         float* d_out, unsigned long long* d_counts, hipStream_t stream);
+hipError_t launch_gamma(const float* d_in, float* d_out, int64_t n, hipStream_t stream);
+// test hooks
+hipError_t launch_debug_math(int fn, const float* x, const float* y, float* out, int64_t n, hipStream_t stream);
+hipError_t launch_debug_log(const DevScene& sc, const FrameParams& fp, int traversal, float* d_out, hipStream_t stream);
+hipError_t launch_debug_trace(const DevScene& sc, int traversal, const float* rays, float* out, int64_t n,
+                              hipStream_t stream);
+
+}  // namespace rt

@@ -1,0 +1,37 @@
+/* rt_debug.h -- test hooks of the native library (not part of the drop-in
+ * boundary).  Used by tests/ to check the device numerics and single-ray
+ * traversal against the CPU oracle. */
+#ifndef RT_DEBUG_H
+#define RT_DEBUG_H
+
+#include <stdint.h>
+#include "rt_api.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Evaluate a function of the numerics contract (rtm.h) on device 0 over host
+ * arrays: fn 0 sin, 1 cos, 2 tan, 3 asin, 4 acos, 5 atan2(x, y), 6 sqrt,
+ * 7 x / y.  y may be NULL for unary functions. */
+int rt_debug_math(rt_ctx* ctx, int fn, const float* x, const float* y, float* out, int64_t n);
+
+/* Trace n rays (rays[6*i..] = dir.xyz, origin.xyz) through the uploaded
+ * scene with the given traversal on device 0; out[2*i] = k, out[2*i+1] =
+ * triangle index (-1 = miss). */
+int rt_debug_trace(rt_ctx* ctx, int traversal, const float* rays, float* out, int64_t n);
+
+/* Render pixel `pixel` of the frame and record its path events (16 floats
+ * each: kind 1 bounce ray / 2 sun ray / 3 sample end, j, o.xyz, d.xyz, k or
+ * -1, material, sampleOut.xyz, 0,0,0), up to cap events, on device 0. */
+int rt_debug_pixel_log(rt_ctx* ctx, int traversal, const float cam[10], const float env[5], int64_t npix, int spp,
+                       int max_bounce, int64_t pixel, float* log, int cap, int* n_events, float out3[3]);
+
+/* Scene facts: out[0] = FAST layout available (1/0), out[1] = FAST stack
+ * depth, out[2] = internal nodes, out[3] = triangles. */
+int rt_debug_scene_info(rt_ctx* ctx, int64_t out[4]);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RT_DEBUG_H */
