@@ -39,20 +39,23 @@ def _newer(target: str, deps) -> bool:
     return any(os.path.getmtime(d) > t for d in deps)
 
 
-def build(verbose: bool = False, force: bool = False) -> str:
+def build(verbose: bool = False, force: bool = False, defines=(), out: str = None) -> str:
+    """Compile the library; ``defines``/``out`` build an experimental variant elsewhere."""
     hipcc = _hipcc()
-    os.makedirs(OBJDIR, exist_ok=True)
-    os.makedirs(LIBDIR, exist_ok=True)
+    lib_path = out or LIB
+    objdir = OBJDIR if not defines else os.path.join(OBJDIR, "v_" + "_".join(d.replace("=", "") for d in defines))
+    os.makedirs(objdir, exist_ok=True)
+    os.makedirs(os.path.dirname(lib_path), exist_ok=True)
     hdrs = [os.path.join(CSRC, h) for h in HEADERS] + [os.path.join(ROOT, "include", h)
                                                       for h in ("rt_api.h", "rt_debug.h")]
     jobs = []
     objs = []
     for src in SOURCES:
         path = os.path.join(CSRC, src)
-        obj = os.path.join(OBJDIR, os.path.splitext(src)[0] + ".o")
+        obj = os.path.join(objdir, os.path.splitext(src)[0] + ".o")
         objs.append(obj)
         if force or _newer(obj, [path] + hdrs):
-            cmd = [hipcc] + COMMON
+            cmd = [hipcc] + COMMON + ["-D" + d for d in defines]
             if src.endswith(".hip"):
                 cmd += ["--offload-arch=gfx950", "-x", "hip"]
             cmd += ["-c", path, "-o", obj]
@@ -68,9 +71,9 @@ def build(verbose: bool = False, force: bool = False) -> str:
 
     with ThreadPoolExecutor(max_workers=min(4, max(1, len(jobs)))) as ex:
         list(ex.map(run, jobs))
-    if force or jobs or _newer(LIB, objs):
-        run([hipcc, "--offload-arch=gfx950", "-shared", "-fPIC", "-o", LIB] + objs)
-    return LIB
+    if force or jobs or _newer(lib_path, objs):
+        run([hipcc, "--offload-arch=gfx950", "-shared", "-fPIC", "-o", lib_path] + objs)
+    return lib_path
 
 
 if __name__ == "__main__":

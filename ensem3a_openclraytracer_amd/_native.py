@@ -47,11 +47,19 @@ def lib():
     with _lock:
         if _lib is not None:
             return _lib
-        if not os.path.exists(LIB):
+        # torch ships its own libamdhip64.so.7 with the same SONAME as ROCm's: whichever is loaded
+        # first serves the whole process.  Load torch's first (when torch is installed) so torch
+        # tensors/streams and this library share ONE HIP runtime.
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
+        lib_path = os.environ.get("ENSEM3A_RT_LIB", LIB)  # experimental variants (tools/variants.py)
+        if not os.path.exists(lib_path):
             raise RuntimeError(
-                f"native library {LIB} is missing: build it with "
+                f"native library {lib_path} is missing: build it with "
                 "`python -m ensem3a_openclraytracer_amd._build` (there is no CPU fallback)")
-        L = ctypes.CDLL(LIB)
+        L = ctypes.CDLL(lib_path)
         sig = {
             "rt_create": (_i32, [_i32, _c_p, ctypes.POINTER(_c_p)]),
             "rt_destroy": (None, [_c_p]),
@@ -167,7 +175,7 @@ class Context:
         c, e = f32(cam), f32(env)
         self._check(lib().rt_render_device(self.handle, int(device_index), ptr(c), ptr(e), int(npix), int(spp),
                                            int(max_bounce), int(row0), int(row_step), _c_p(int(d_out_ptr)),
-                                           _c_p(int(stream_ptr)) if stream_ptr else None))
+                                           _c_p(int(stream_ptr)) if stream_ptr else None))  # 0 = default stream
 
     def count_work(self, cam, env, npix, spp, max_bounce, row0=0, row_step=1):
         c, e = f32(cam), f32(env)

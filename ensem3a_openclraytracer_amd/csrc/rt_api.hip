@@ -34,7 +34,7 @@ struct DevBuf {
 struct Device {
     int id = 0;
     hipStream_t stream = nullptr;
-    DevBuf nodes, bvh9, tri_geo, tri_shade, mat, ibl, out, counts, scratch_a, scratch_b;
+    DevBuf nodes, bvh9, tri_geo, tri_shade, tri_frame, mat, ibl, out, counts, work, scratch_a, scratch_b;
     float* host_stage = nullptr;  // pinned staging for rt_render
     size_t host_stage_bytes = 0;
 };
@@ -236,6 +236,7 @@ rt::DevScene dev_scene(const rt_ctx* ctx, const Device& d) {
     s.nbvh9 = ctx->hs.nbvh9;
     s.tri_geo = (const float4*)d.tri_geo.p;
     s.tri_shade = (const float4*)d.tri_shade.p;
+    s.tri_frame = (const float4*)d.tri_frame.p;
     s.ntri = ctx->hs.ntri;
     s.mat = (const float*)d.mat.p;
     s.nmat = ctx->hs.nmat;
@@ -320,8 +321,8 @@ void rt_destroy(rt_ctx* ctx) {
     for (auto& d : ctx->devs) {
         if (hipSetDevice(d.id) != hipSuccess) continue;
         if (d.stream) (void)hipStreamSynchronize(d.stream);
-        for (DevBuf* b : {&d.nodes, &d.bvh9, &d.tri_geo, &d.tri_shade, &d.mat, &d.ibl, &d.out, &d.counts,
-                          &d.scratch_a, &d.scratch_b})
+        for (DevBuf* b : {&d.nodes, &d.bvh9, &d.tri_geo, &d.tri_shade, &d.tri_frame, &d.mat, &d.ibl, &d.out,
+                          &d.counts, &d.work, &d.scratch_a, &d.scratch_b})
             release(*b);
         if (d.host_stage) (void)hipHostFree(d.host_stage);
         if (d.stream) (void)hipStreamDestroy(d.stream);
@@ -428,7 +429,7 @@ int rt_set_scene(rt_ctx* ctx, const float* vp, int64_t nvp, const float* vn, int
     std::string why;
     hs.fast_ok = (T > 0) ? pack_fast(hs, bvh9, NB, T, why) : true;
     if (T == 0) { hs.nnodes = 0; hs.root_ref = 0; hs.depth = 1; }
-    if (hs.fast_ok && (int64_t)hs.depth * 256 * 4 > 64 * 1024) {
+    if (hs.fast_ok && (int64_t)hs.depth * 256 * 8 > 64 * 1024) {  // int2 stack entries, block <= 256
         hs.fast_ok = false;
         why = "tree too deep for the LDS stack";
     }
@@ -440,9 +441,16 @@ int rt_set_scene(rt_ctx* ctx, const float* vp, int64_t nvp, const float* vn, int
         HIP_OR_RET(ctx, upload(d.tri_geo, hs.tri_geo, d.stream));
         HIP_OR_RET(ctx, upload(d.tri_shade, hs.tri_shade, d.stream));
         HIP_OR_RET(ctx, upload(d.mat, hs.mat, d.stream));
+        HIP_OR_RET(ctx, ensure(d.tri_frame, (size_t)std::max<int64_t>(T, 1) * 3 * sizeof(float4)));
+        HIP_OR_RET(ctx, ensure(d.work, 1024));
         HIP_OR_RET(ctx, hipStreamSynchronize(d.stream));
     }
     ctx->hs = std::move(hs);
+    for (auto& d : ctx->devs) {
+        HIP_OR_RET(ctx, hipSetDevice(d.id));
+        HIP_OR_RET(ctx, rt::launch_prep_frames(dev_scene(ctx, d), (float4*)d.tri_frame.p, d.stream));
+        HIP_OR_RET(ctx, hipStreamSynchronize(d.stream));
+    }
     ctx->have_scene = true;
     if (!ctx->hs.fast_ok) ctx->err = "FAST traversal unavailable (" + why + "); REF traversal will be used";
     return RT_OK;
@@ -483,8 +491,9 @@ int rt_render_device(rt_ctx* ctx, int device_index, const float cam[10], const f
     fp.max_bounce = max_bounce;
     Device& d = ctx->devs[device_index];
     HIP_OR_RET(ctx, hipSetDevice(d.id));
-    hipStream_t s = stream ? (hipStream_t)stream : d.stream;
-    HIP_OR_RET(ctx, rt::launch_render(dev_scene(ctx, d), fp, effective_traversal(ctx), ctx->block, d_out, nullptr, s));
+    hipStream_t s = (hipStream_t)stream;  // NULL = the device's default (null) stream, HIP convention
+    HIP_OR_RET(ctx, rt::launch_render(dev_scene(ctx, d), fp, effective_traversal(ctx), ctx->block, d_out, nullptr,
+                                      (unsigned int*)d.work.p, s));
     return RT_OK;
 }
 
@@ -517,7 +526,7 @@ int rt_render(rt_ctx* ctx, const float cam[10], const float env[5], int64_t npix
             d.host_stage_bytes = bytes;
         }
         HIP_OR_RET(ctx, rt::launch_render(dev_scene(ctx, d), fp, effective_traversal(ctx), ctx->block,
-                                          (float*)d.out.p, nullptr, d.stream));
+                                          (float*)d.out.p, nullptr, (unsigned int*)d.work.p, d.stream));
         HIP_OR_RET(ctx, hipMemcpyAsync(d.host_stage, d.out.p, bytes, hipMemcpyDeviceToHost, d.stream));
     }
     for (int k = 0; k < nd; ++k) {
@@ -554,7 +563,7 @@ int rt_count_work(rt_ctx* ctx, const float cam[10], const float env[5], int64_t 
     HIP_OR_RET(ctx, ensure(d.counts, 5 * sizeof(unsigned long long)));
     HIP_OR_RET(ctx, hipMemsetAsync(d.counts.p, 0, 5 * sizeof(unsigned long long), d.stream));
     HIP_OR_RET(ctx, rt::launch_render(dev_scene(ctx, d), fp, effective_traversal(ctx), ctx->block, (float*)d.out.p,
-                                      (unsigned long long*)d.counts.p, d.stream));
+                                      (unsigned long long*)d.counts.p, (unsigned int*)d.work.p, d.stream));
     unsigned long long h[5];
     HIP_OR_RET(ctx, hipMemcpyAsync(h, d.counts.p, sizeof h, hipMemcpyDeviceToHost, d.stream));
     HIP_OR_RET(ctx, hipStreamSynchronize(d.stream));
@@ -650,7 +659,7 @@ int rt_debug_pixel_log(rt_ctx* ctx, int traversal, const float cam[10], const fl
     fp.log_cap = cap;
     fp.log_pixel = pixel;
     HIP_OR_RET(ctx, hipMemsetAsync(fp.log_count, 0, sizeof(int32_t), d.stream));
-    HIP_OR_RET(ctx, rt::launch_debug_log(dev_scene(ctx, d), fp, traversal, dout, d.stream));
+    HIP_OR_RET(ctx, rt::launch_debug_log(dev_scene(ctx, d), fp, traversal, dout, (unsigned int*)d.work.p, d.stream));
     int32_t n = 0;
     HIP_OR_RET(ctx, hipMemcpyAsync(&n, fp.log_count, sizeof n, hipMemcpyDeviceToHost, d.stream));
     HIP_OR_RET(ctx, hipStreamSynchronize(d.stream));

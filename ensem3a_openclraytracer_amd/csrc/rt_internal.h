@@ -24,6 +24,8 @@ struct DevScene {
     const float4* tri_geo;
     // hit record per triangle: first-vertex normal | material index bits
     const float4* tri_shade;
+    // hemisphere frame per triangle (prep_frames_kernel): q, qinv, normalize(n) | colinear flag
+    const float4* tri_frame;
     int32_t ntri;
     // materials: 6 floats each [type, r, g, b, roughness, ior]
     const float* mat;
@@ -52,12 +54,16 @@ struct FrameParams {
 
 // Launch the render kernel; counts != nullptr selects the instrumented build
 // (device pointer to 5 uint64 accumulators).
+// d_work: >= 512 bytes of device scratch: the persistent kernel's pixel counter (zeroed by the
+// launch) followed by the per-launch constants block.
 hipError_t launch_render(const DevScene& sc, const FrameParams& fp, int traversal, int block,
-                         float* d_out, unsigned long long* d_counts, hipStream_t stream);
+                         float* d_out, unsigned long long* d_counts, unsigned int* d_work, hipStream_t stream);
+hipError_t launch_prep_frames(const DevScene& sc, float4* frame, hipStream_t stream);
 hipError_t launch_gamma(const float* d_in, float* d_out, int64_t n, hipStream_t stream);
 // test hooks
 hipError_t launch_debug_math(int fn, const float* x, const float* y, float* out, int64_t n, hipStream_t stream);
-hipError_t launch_debug_log(const DevScene& sc, const FrameParams& fp, int traversal, float* d_out, hipStream_t stream);
+hipError_t launch_debug_log(const DevScene& sc, const FrameParams& fp, int traversal, float* d_out,
+                            unsigned int* d_work, hipStream_t stream);
 hipError_t launch_debug_trace(const DevScene& sc, int traversal, const float* rays, float* out, int64_t n,
                               hipStream_t stream);
 

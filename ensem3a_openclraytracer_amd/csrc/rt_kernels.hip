@@ -24,6 +24,8 @@
 //
 // Numerics: every OpenCL builtin of the reference is taken from rtm.h and the
 // file is compiled with -ffp-contract=off (see rtm.h).
+#include <algorithm>
+
 #include "rt_internal.h"
 #include "rtm.h"
 
@@ -120,80 +122,122 @@ __device__ Hit trace_ref(const DevScene& S, rtm_f3 o, rtm_f3 d, int* __restrict_
 }
 
 // ---- FAST traversal ----
-__device__ __forceinline__ void slab(float lo_x, float hi_x, float lo_y, float hi_y, float lo_z, float hi_z,
-                                     float ox, float oy, float oz, float ix, float iy, float iz,
-                                     float& tmin, float& tmax) {
+// Slab test of one box against a ray given as inv = 1/d (and oi = o*inv).
+// RT_SLAB_FMA=1 uses one fma per plane, t = b*inv - o*inv, which cancels badly
+// when a direction component is tiny (|o/d| large); the default keeps the
+// reference's (b - o) scaled by 1/d.
+#ifndef RT_SLAB_FMA
+#define RT_SLAB_FMA 0
+#endif
+__device__ __forceinline__ void slab_fma(float lo_x, float hi_x, float lo_y, float hi_y, float lo_z, float hi_z,
+                                         float ox, float oy, float oz, float ix, float iy, float iz, float oix,
+                                         float oiy, float oiz, float& tmin, float& tmax) {
+#if RT_SLAB_FMA
+    const float x0 = fmaf(lo_x, ix, -oix), x1 = fmaf(hi_x, ix, -oix);
+    const float y0 = fmaf(lo_y, iy, -oiy), y1 = fmaf(hi_y, iy, -oiy);
+    const float z0 = fmaf(lo_z, iz, -oiz), z1 = fmaf(hi_z, iz, -oiz);
+#else
     const float x0 = (lo_x - ox) * ix, x1 = (hi_x - ox) * ix;
     const float y0 = (lo_y - oy) * iy, y1 = (hi_y - oy) * iy;
     const float z0 = (lo_z - oz) * iz, z1 = (hi_z - oz) * iz;
+#endif
     tmin = fmaxf(fmaxf(fminf(x0, x1), fminf(y0, y1)), fminf(z0, z1));
     tmax = fminf(fminf(fmaxf(x0, x1), fmaxf(y0, y1)), fmaxf(z0, z1));
 }
 
 constexpr float CULL_MARGIN = 1.0f + 0x1p-12f;
 
-template <bool COUNT>
-__device__ __forceinline__ void fast_leaf(const DevScene& S, int t, rtm_f3 o, rtm_f3 d, Hit& best, int& best_rank,
-                                          Cnt& c) {
-    if (COUNT) c.tris++;
-    float k;
-    int rank;
-    if (mt_test(S.tri_geo, t, o, d, &k, &rank) && k > 0.0001f &&
-        (k < best.k || (k == best.k && rank < best_rank))) {
-        best.k = k;
-        best.tri = t;
-        best_rank = rank;
-    }
+// Branch-free Moller-Trumbore (same arithmetic as mt_test): all three loads are
+// issued together and one predicate decides, so a wave pays one memory round trip
+// and no nested divergence per triangle.
+__device__ __forceinline__ bool mt_flat(const float4* __restrict__ tg, int t, rtm_f3 o, rtm_f3 d, float* kout,
+                                        int* rank) {
+    const float4 g0 = tg[3 * t + 0];
+    const float4 g1 = tg[3 * t + 1];
+    const float4 g2 = tg[3 * t + 2];
+    const rtm_f3 e1 = xyz(g1), e2 = xyz(g2);
+    const rtm_f3 h = rtm_cross(d, e2);
+    const float a = rtm_dot(e1, h);
+    const float f = 1.0f / a;
+    const rtm_f3 s = rtm_sub(o, xyz(g0));
+    const float u = f * rtm_dot(s, h);
+    const rtm_f3 q = rtm_cross(s, e1);
+    const float v = f * rtm_dot(d, q);
+    const float k = f * rtm_dot(e2, q);
+    *kout = k;
+    *rank = __float_as_int(g0.w);
+    const bool parallel = a > -0.0000001f && a < 0.0000001f;
+    return !parallel && !(u < 0.0f || u > 1.0f) && !(v < 0.0f || u + v > 1.0f) && (k > 0.0000001f);
 }
 
+// One item per iteration: an internal node (both child boxes tested, nearer hit
+// child continues, the farther is pushed with its entry distance) or a leaf
+// (one triangle test).  Popped items whose entry distance is beyond the best hit
+// are discarded without a fetch.  Stack entries: int2 (ref, tmin bits) in LDS.
 template <bool COUNT>
-__device__ Hit trace_fast(const DevScene& S, rtm_f3 o, rtm_f3 d, int* __restrict__ stk, int B, Cnt& c) {
+__device__ Hit trace_fast(const DevScene& S, rtm_f3 o, rtm_f3 d, int* __restrict__ stk_base, int B, Cnt& c) {
     Hit best{1000.0f, -1};
     int best_rank = -1;
     if (COUNT) c.rays++;
     if (S.ntri <= 0) return best;
+    int2* __restrict__ stk = reinterpret_cast<int2*>(stk_base - threadIdx.x) + threadIdx.x;
     const float ix = 1.0f / d.x, iy = 1.0f / d.y, iz = 1.0f / d.z;
+    const float oix = o.x * ix, oiy = o.y * iy, oiz = o.z * iz;
     float tmin, tmax;
-    slab(S.root_box[0], S.root_box[3], S.root_box[1], S.root_box[4], S.root_box[2], S.root_box[5], o.x, o.y, o.z,
-         ix, iy, iz, tmin, tmax);
+    slab_fma(S.root_box[0], S.root_box[3], S.root_box[1], S.root_box[4], S.root_box[2], S.root_box[5], o.x, o.y, o.z,
+             ix, iy, iz, oix, oiy, oiz, tmin, tmax);
     if (!(tmax >= tmin && tmax >= 0.0f)) return best;
-    if (S.root_ref < 0) {
-        fast_leaf<COUNT>(S, ~S.root_ref, o, d, best, best_rank, c);
-        return best;
-    }
-    int node = S.root_ref;
+    int item = S.root_ref;
     int sp = 0;
     const float4* __restrict__ nodes = S.nodes;
     while (true) {
-        if (COUNT) c.nodes++;
-        const float4 a = nodes[4 * node + 0];
-        const float4 b = nodes[4 * node + 1];
-        const float4 z = nodes[4 * node + 2];
-        const float4 e = nodes[4 * node + 3];
-        float t0n, t0x, t1n, t1x;
-        slab(a.x, a.y, a.z, a.w, z.x, z.y, o.x, o.y, o.z, ix, iy, iz, t0n, t0x);
-        slab(b.x, b.y, b.z, b.w, z.z, z.w, o.x, o.y, o.z, ix, iy, iz, t1n, t1x);
-        const int r0 = __float_as_int(e.x), r1 = __float_as_int(e.y);
-        const float cull = best.k * CULL_MARGIN;
-        const bool h0 = t0x >= t0n && t0x >= 0.0f && t0n <= cull;
-        const bool h1 = t1x >= t1n && t1x >= 0.0f && t1n <= cull;
-        if (h0 && r0 < 0) fast_leaf<COUNT>(S, ~r0, o, d, best, best_rank, c);
-        if (h1 && r1 < 0) fast_leaf<COUNT>(S, ~r1, o, d, best, best_rank, c);
-        const bool i0 = h0 && r0 >= 0, i1 = h1 && r1 >= 0;
-        if (i0 && i1) {
-            const bool first0 = t0n <= t1n;
-            stk[sp * B] = first0 ? r1 : r0;
-            ++sp;
-            node = first0 ? r0 : r1;
-        } else if (i0) {
-            node = r0;
-        } else if (i1) {
-            node = r1;
+        if (item >= 0) {
+            if (COUNT) c.nodes++;
+            const float4 a = nodes[4 * item + 0];
+            const float4 b = nodes[4 * item + 1];
+            const float4 z = nodes[4 * item + 2];
+            const float4 e = nodes[4 * item + 3];
+            float t0n, t0x, t1n, t1x;
+            slab_fma(a.x, a.y, a.z, a.w, z.x, z.y, o.x, o.y, o.z, ix, iy, iz, oix, oiy, oiz, t0n, t0x);
+            slab_fma(b.x, b.y, b.z, b.w, z.z, z.w, o.x, o.y, o.z, ix, iy, iz, oix, oiy, oiz, t1n, t1x);
+            const float cull = best.k * CULL_MARGIN;
+            const bool h0 = t0x >= t0n && t0x >= 0.0f && t0n <= cull;
+            const bool h1 = t1x >= t1n && t1x >= 0.0f && t1n <= cull;
+            const int r0 = __float_as_int(e.x), r1 = __float_as_int(e.y);
+            if (h0 && h1) {
+                const bool first0 = t0n <= t1n;
+                stk[sp * B] = make_int2(first0 ? r1 : r0, __float_as_int(first0 ? t1n : t0n));
+                ++sp;
+                item = first0 ? r0 : r1;
+                continue;
+            }
+            if (h0 || h1) {
+                item = h0 ? r0 : r1;
+                continue;
+            }
         } else {
-            if (sp == 0) break;
-            --sp;
-            node = stk[sp * B];
+            if (COUNT) c.tris++;
+            float k;
+            int rank;
+            const int t = ~item;
+            if (mt_flat(S.tri_geo, t, o, d, &k, &rank) && k > 0.0001f &&
+                (k < best.k || (k == best.k && rank < best_rank))) {
+                best.k = k;
+                best.tri = t;
+                best_rank = rank;
+            }
         }
+        // pop the next item still in front of the best hit
+        item = 0x7fffffff;
+        while (sp > 0) {
+            --sp;
+            const int2 en = stk[sp * B];
+            if (__int_as_float(en.y) <= best.k * CULL_MARGIN) {
+                item = en.x;
+                break;
+            }
+        }
+        if (item == 0x7fffffff) break;
     }
     return best;
 }
@@ -204,38 +248,67 @@ __device__ __forceinline__ Hit trace(const DevScene& S, rtm_f3 o, rtm_f3 d, int*
     return trace_fast<COUNT>(S, o, d, stk, B, c);
 }
 
-// ---- camera, Raytracing.cl:18-37 ----
-__device__ __forceinline__ void gen_camera_ray(const float* cam, int i, rtm_f3& o, rtm_f3& d) {
-    const int W = (int)cam[6];
+// ---- per-launch constants (Raytracing.cl:18-37, 115-118; MathLib.cl:72-80) ----
+// Every rotation whose angle and axis do not depend on the pixel is prepared
+// once per thread with rtm_rot_prepare, then applied with rtm_rot_apply: the
+// same arithmetic as the reference's rotateVec, done once instead of per call.
+struct LaunchConst {
+    rtm_rot cam_rx, cam_ry, cam_rz;   // genCameraRay rotations
+    rtm_rot ibl_x, ibl_y;             // SampleSphericalMap's 90 degree rotations
+    rtm_f3 focal, position, sun;      // camera focal point and origin, unnormalised sun vector
+    float pas;                        // 1.0 / cam[6]
+};
+
+__device__ __forceinline__ LaunchConst make_const(const FrameParams& F) {  // evaluated once per launch
+    LaunchConst c;
+    const float* cam = F.cam;
+    c.focal = rtm_v3(cam[0], cam[1] - (1.0f / (2.0f * rtm_tan(cam[9] / 2.0f))), cam[2]);
+    c.position = rtm_v3(cam[0], cam[1], cam[2]);
+    c.pas = 1.0f / cam[6];
+    c.cam_rx = rtm_rot_prepare(cam[3] * (3.14f / 180.0f), rtm_v3(1, 0, 0));
+    c.cam_ry = rtm_rot_prepare(cam[4] * (3.14f / 180.0f), rtm_v3(0, 1, 0));
+    c.cam_rz = rtm_rot_prepare(cam[5] * (3.14f / 180.0f), rtm_v3(0, 0, 1));
+    c.ibl_x = rtm_rot_prepare(90.0f * (3.14f / 180.0f), rtm_v3(1, 0, 0));
+    c.ibl_y = rtm_rot_prepare(90.0f * (3.14f / 180.0f), rtm_v3(0, 1, 0));
+    rtm_f3 sun = rtm_v3(1, 1, 1);
+    sun = rtm_rotate(F.env[0] * (3.14f / 180.0f), rtm_v3(1, 0, 0), sun);
+    sun = rtm_rotate(F.env[1] * (3.14f / 180.0f), rtm_v3(0, 1, 0), sun);
+    sun = rtm_rotate(F.env[2] * (3.14f / 180.0f), rtm_v3(0, 0, 1), sun);
+    c.sun = sun;
+    return c;
+}
+
+__global__ void make_const_kernel(FrameParams F, LaunchConst* __restrict__ out) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) *out = make_const(F);
+}
+
+// ---- camera ray direction, Raytracing.cl:18-37 ----
+__device__ __forceinline__ rtm_f3 camera_dir(const LaunchConst& C, int W, int i) {
     const int pixelY = (i + 1) % W;
     const int pixelX = (i - pixelY) / W;
-    const rtm_f3 focal = rtm_v3(cam[0], cam[1] - (1.0f / (2.0f * rtm_tan(cam[9] / 2.0f))), cam[2]);
-    const rtm_f3 position = rtm_v3(cam[0], cam[1], cam[2]);
-    const float pas = 1.0f / cam[6];
-    const rtm_f3 pc = rtm_v3(fmaf((float)pixelY, pas, -0.5f), 0.0f, fmaf(-(float)pixelX, pas, 0.5f));
-    o = position;
-    d = rtm_normalize(rtm_sub(rtm_add(position, pc), focal));
-    d = rtm_rotate(cam[3] * (3.14f / 180.0f), rtm_v3(1, 0, 0), d);
-    d = rtm_rotate(cam[4] * (3.14f / 180.0f), rtm_v3(0, 1, 0), d);
-    d = rtm_rotate(cam[5] * (3.14f / 180.0f), rtm_v3(0, 0, 1), d);
+    const rtm_f3 pc = rtm_v3(fmaf((float)pixelY, C.pas, -0.5f), 0.0f, fmaf(-(float)pixelX, C.pas, 0.5f));
+    rtm_f3 d = rtm_normalize(rtm_sub(rtm_add(C.position, pc), C.focal));
+    d = rtm_rot_apply(C.cam_rx, d);
+    d = rtm_rot_apply(C.cam_ry, d);
+    return rtm_rot_apply(C.cam_rz, d);
 }
 
 // ---- IBL, MathLib.cl:72-90 (integer coords through a linear sampler) ----
 template <bool COUNT>
-__device__ rtm_f3 sample_ibl(const DevScene& S, rtm_f3 dir, Cnt& c) {
+__device__ rtm_f3 sample_ibl(const DevScene& S, const LaunchConst& C, rtm_f3 dir, Cnt& c) {
     if (COUNT) c.env++;
-    dir = rtm_rotate(90.0f * (3.14f / 180.0f), rtm_v3(1, 0, 0), dir);
-    dir = rtm_rotate(90.0f * (3.14f / 180.0f), rtm_v3(0, 1, 0), dir);
+    dir = rtm_rot_apply(C.ibl_x, dir);
+    dir = rtm_rot_apply(C.ibl_y, dir);
     float u = rtm_atan2(dir.z, dir.x), v = rtm_asin(dir.y);
     u = u * 0.1591f;
     v = v * 0.3183f;
     u = u + 0.5f;
     v = v + 0.5f;
     const int W = S.ibl_w, H = S.ibl_h;
-    const int x = (int)(u * (float)W);
-    const int y = (int)(v * (float)H);
-    const int x0 = min(max(x - 1, 0), W - 1), x1 = min(max(x, 0), W - 1);
-    const int y0 = min(max(y - 1, 0), H - 1), y1 = min(max(y, 0), H - 1);
+    const int x = rtm_f2i(u * (float)W);
+    const int y = rtm_f2i(v * (float)H);
+    const int x0 = min(max(x > -2147483647 ? x - 1 : x, 0), W - 1), x1 = min(max(x, 0), W - 1);
+    const int y0 = min(max(y > -2147483647 ? y - 1 : y, 0), H - 1), y1 = min(max(y, 0), H - 1);
     const uchar4 t00 = S.ibl[(int64_t)y0 * W + x0];
     const uchar4 t10 = S.ibl[(int64_t)y0 * W + x1];
     const uchar4 t01 = S.ibl[(int64_t)y1 * W + x0];
@@ -247,8 +320,11 @@ __device__ rtm_f3 sample_ibl(const DevScene& S, rtm_f3 dir, Cnt& c) {
     return rtm_scale(rtm_v3(sr * w, sg * w, sb * w), 1.0f);
 }
 
-// ---- samplers, MathLib.cl:313-366 ----
-__device__ __forceinline__ rtm_f3 hemi_cosine(rtm_f3 dir, uint32_t* s0, uint32_t* s1, float* invPdf) {
+// ---- hemisphere samplers, MathLib.cl:313-366, with the triangle's frame
+// (colinear flag, rotation to the normal, normalize(n)) precomputed by
+// prep_frames_kernel: f0/f1 = q/qinv of the rotation, f2 = normalize(n) | colinear ----
+__device__ __forceinline__ rtm_f3 hemi_cosine(rtm_f3 n, float4 f0, float4 f1, float4 f2, uint32_t* s0,
+                                              uint32_t* s1, float* invPdf) {
     const float u = rtm_rand(s0, s1);
     const float theta = rtm_rand(s0, s1) * 2.0f * 3.14f;
     const float r = sqrtf(u);
@@ -256,19 +332,20 @@ __device__ __forceinline__ rtm_f3 hemi_cosine(rtm_f3 dir, uint32_t* s0, uint32_t
     rtm_sincos(theta, &st, &ct);
     const rtm_f3 localV = rtm_v3(r * ct, r * st, sqrtf(rtm_fmax(0.0f, 1.0f - u)));
     rtm_f3 l;
-    const float colinear = rtm_fabs(rtm_dot(rtm_normalize(dir), rtm_v3(0.0f, 0.0f, 1.0f)));
-    if (colinear == 1.0f) {
-        l = rtm_scale(localV, dir.z);
+    if (f2.w != 0.0f) {
+        l = rtm_scale(localV, n.z);
     } else {
-        const rtm_f3 axis = rtm_cross(rtm_v3(0, 0, 1), dir);
-        const float ang = rtm_acos(rtm_dot(dir, rtm_v3(0, 0, 1)));
-        l = rtm_normalize(rtm_rotate(ang, axis, localV));
+        rtm_rot R;
+        R.q = rtm_v4(f0.x, f0.y, f0.z, f0.w);
+        R.qinv = rtm_v4(f1.x, f1.y, f1.z, f1.w);
+        l = rtm_normalize(rtm_rot_apply(R, localV));
     }
-    *invPdf = 3.14f / (rtm_fmax(rtm_dot(l, dir), 0.0f));
+    *invPdf = 3.14f / (rtm_fmax(rtm_dot(l, n), 0.0f));
     return l;
 }
 
-__device__ __forceinline__ rtm_f3 hemi_uniform(rtm_f3 dir, uint32_t* s0, uint32_t* s1, float* invPdf) {
+__device__ __forceinline__ rtm_f3 hemi_uniform(rtm_f3 n, float4 f0, float4 f1, float4 f2, uint32_t* s0,
+                                               uint32_t* s1, float* invPdf) {
     const float phi = 2.0f * 3.14f * (rtm_rand(s0, s1));
     const float theta = rtm_acos(1.0f - (rtm_rand(s0, s1)));
     float sp, cp, sth, cth;
@@ -276,13 +353,13 @@ __device__ __forceinline__ rtm_f3 hemi_uniform(rtm_f3 dir, uint32_t* s0, uint32_
     rtm_sincos(theta, &sth, &cth);
     const rtm_f3 localV = rtm_v3(cp * sth, sth * sp, cth);
     rtm_f3 w;
-    const float colinear = rtm_fabs(rtm_dot(rtm_normalize(dir), rtm_v3(0.0f, 0.0f, 1.0f)));
-    if (colinear == 1.0f) {
-        w = rtm_scale(localV, dir.z);
+    if (f2.w != 0.0f) {
+        w = rtm_scale(localV, n.z);
     } else {
-        const rtm_f3 axis = rtm_normalize(rtm_cross(rtm_v3(0.0f, 0.0f, 1.0f), dir));
-        const float ang = rtm_acos(rtm_dot(dir, rtm_v3(0, 0, 1.0f)));
-        w = rtm_rotate(ang, axis, localV);
+        rtm_rot R;
+        R.q = rtm_v4(f0.x, f0.y, f0.z, f0.w);
+        R.qinv = rtm_v4(f1.x, f1.y, f1.z, f1.w);
+        w = rtm_rot_apply(R, localV);
     }
     *invPdf = 2.0f * 3.14f;
     return w;
@@ -329,7 +406,30 @@ __device__ __forceinline__ Mat load_mat(const float* __restrict__ m, int idx) {
     return r;
 }
 
-enum Phase { PREP = 0, BOUNCE = 1, SUN = 2 };
+// Per-triangle hemisphere frame: the rotation rand_hemi_cosine / rand_hemi_uniform
+// (MathLib.cl:325-336, 349-362) build from the hit normal, which only depends on
+// the triangle.  Computed on the device with the same rtm_* arithmetic.
+__global__ void prep_frames_kernel(const float4* __restrict__ tri_shade, const float* __restrict__ mat, int ntri,
+                                   float4* __restrict__ frame) {
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= ntri) return;
+    const float4 sh = tri_shade[t];
+    const rtm_f3 n = xyz(sh);
+    const int type = (int)mat[6 * __float_as_int(sh.w)];
+    const rtm_f3 nn = rtm_normalize(n);
+    const float colinear = rtm_fabs(rtm_dot(nn, rtm_v3(0.0f, 0.0f, 1.0f)));
+    rtm_rot R;
+    R.q = rtm_v4(1, 0, 0, 0);
+    R.qinv = R.q;
+    if (colinear != 1.0f) {
+        const float ang = rtm_acos(rtm_dot(n, rtm_v3(0, 0, 1)));
+        if (type == 1) R = rtm_rot_prepare(ang, rtm_cross(rtm_v3(0, 0, 1), n));
+        else if (type == 2) R = rtm_rot_prepare(ang, rtm_normalize(rtm_cross(rtm_v3(0.0f, 0.0f, 1.0f), n)));
+    }
+    frame[3 * t + 0] = make_float4(R.q.x, R.q.y, R.q.z, R.q.w);
+    frame[3 * t + 1] = make_float4(R.qinv.x, R.qinv.y, R.qinv.z, R.qinv.w);
+    frame[3 * t + 2] = make_float4(nn.x, nn.y, nn.z, colinear == 1.0f ? 1.0f : 0.0f);
+}
 
 __device__ __forceinline__ void log_event(const FrameParams& F, float kind, int j, rtm_f3 o, rtm_f3 d, float k,
                                           int mat, rtm_f3 so) {
@@ -341,156 +441,215 @@ __device__ __forceinline__ void log_event(const FrameParams& F, float kind, int 
     *F.log_count = n + 1;
 }
 
+enum Phase { FETCH = 0, PRIMARY = 1, PREP = 2, BOUNCE = 3, SUN = 4, DONE = 5 };
+
+// One persistent lane = one pixel at a time.  Lanes that finish their pixel
+// take the next pixel index from a global counter: the wave ballots the lanes
+// that need work, one lane adds the count to the counter, and each lane takes
+// base + (its rank among the requesting lanes) -- so no lane idles while the
+// rest of its wave finishes a slower pixel.  Per loop iteration every busy
+// lane traces exactly one ray (primary, bounce or sun ray).
 template <int TRAV, bool COUNT, bool LOG = false>
 __global__ void __launch_bounds__(256) render_kernel(DevScene S, FrameParams F, float* __restrict__ out,
-                                                     unsigned long long* __restrict__ counts) {
+                                                     unsigned long long* __restrict__ counts,
+                                                     unsigned int* __restrict__ work_counter,
+                                                     const LaunchConst* __restrict__ lconst) {
     extern __shared__ int lds_stack[];
     const int B = blockDim.x;
     int* stk = lds_stack + threadIdx.x;
     Cnt c{0, 0, 0, 0, 0};
-    const int64_t p = (int64_t)blockIdx.x * B + threadIdx.x;
-    bool active = p < F.nloc;
-    int i = 0;
-    if (active) {
-        const int64_t krow = p / F.width;
-        const int64_t col = p - krow * F.width;
-        const int64_t i64 = ((int64_t)F.row0 + krow * F.row_step) * F.width + col;
-        active = i64 < F.npix;
-        i = (int)i64;
-    }
-    const bool logme = LOG && active && i == F.log_pixel;
-    if (active) {
-        const int imgSize = (int)F.npix;
-        uint32_t seed0 = (uint32_t)(i % imgSize);
-        uint32_t seed1 = (uint32_t)(i / imgSize);
-        const float e3 = F.env[3], e4 = F.env[4];
+    const LaunchConst& C = *lconst;   // uniform: scalar loads, no VGPRs
+    const int W = F.width;
+    const int imgSize = (int)F.npix;
+    const float e3 = F.env[3], e4 = F.env[4];
+    const int spp = F.spp, maxB = F.max_bounce;
+    const unsigned int nloc = (unsigned int)F.nloc;
+    const int lane = threadIdx.x & 63;
 
-        rtm_f3 co, cd;
-        gen_camera_ray(F.cam, i, co, cd);
-        const Hit hc = trace<TRAV, COUNT>(S, co, cd, stk, B, c);
-        const bool hitc = hc.tri >= 0;
-        rtm_f3 nc = rtm_v3(0, 0, 0);
-        int mc = 0;
-        if (hitc) {
-            const float4 sh = S.tri_shade[hc.tri];
-            nc = xyz(sh);
-            mc = __float_as_int(sh.w);
+    int phase = FETCH;
+    int p = 0, i = 0;
+    bool logme = false;
+    uint32_t seed0 = 0, seed1 = 0;
+    rtm_f3 cd = rtm_v3(0, 0, 0);              // camera ray direction (origin = C.position)
+    float kc = 1000.0f;                       // cached primary hit
+    int tc = -1;
+    rtm_f3 Ro = rtm_v3(0, 0, 0), Rd = rtm_v3(0, 0, 0), so = rtm_v3(1, 1, 1);
+    float k = 1000.0f;
+    int tri = -1, j = 0;
+    rtm_f3 Bo = rtm_v3(0, 0, 0), Bd = rtm_v3(0, 0, 0);
+    rtm_f3 acc = rtm_v3(0, 0, 0);
+    int s = 0;
+
+    while (true) {
+        // -- refill: ballot the lanes that need a pixel, one atomic per wave --
+        const unsigned long long need = __ballot(phase == FETCH);
+        if (need) {
+            unsigned int base = 0;
+            const int leader = __ffsll((long long)need) - 1;
+            if (lane == leader) base = atomicAdd(work_counter, (unsigned int)__popcll(need));
+            base = __shfl(base, leader, 64);
+            if (phase == FETCH) {
+                const unsigned long long below = need & ((1ull << lane) - 1ull);
+                const unsigned int q = base + (unsigned int)__popcll(below);
+                bool ok = q < nloc;
+                if (ok) {
+                    p = (int)q;
+                    const int krow = p / W;
+                    const int col = p - krow * W;
+                    const int64_t i64 = ((int64_t)F.row0 + (int64_t)krow * F.row_step) * W + col;
+                    ok = i64 < F.npix;
+                    i = (int)i64;
+                }
+                if (ok) {
+                    seed0 = (uint32_t)(i % imgSize);
+                    seed1 = (uint32_t)(i / imgSize);
+                    cd = camera_dir(C, W, i);
+                    acc = rtm_v3(0, 0, 0);
+                    s = 0;
+                    phase = PRIMARY;
+                    logme = LOG && i == F.log_pixel;
+                } else {
+                    phase = DONE;
+                }
+            }
         }
-        // sun direction (Raytracing.cl:115-118), unnormalised
-        rtm_f3 sun = rtm_v3(1, 1, 1);
-        sun = rtm_rotate(F.env[0] * (3.14f / 180.0f), rtm_v3(1, 0, 0), sun);
-        sun = rtm_rotate(F.env[1] * (3.14f / 180.0f), rtm_v3(0, 1, 0), sun);
-        sun = rtm_rotate(F.env[2] * (3.14f / 180.0f), rtm_v3(0, 0, 1), sun);
+        if (__all(phase == DONE)) break;
+        if (phase == DONE) continue;
 
-        // path state: the reference's (R_cam, H_cam, camMat, j, sampleOut)
-        rtm_f3 Ro = co, Rd = cd, n = nc, so = rtm_v3(1, 1, 1);
-        bool hit = hitc;
-        float k = hc.k;
-        int mid = mc, j = 0;
-        rtm_f3 Bo = rtm_v3(0, 0, 0), Bd = rtm_v3(0, 0, 0);  // pending bounce ray
-        rtm_f3 acc = rtm_v3(0, 0, 0);
-        int s = 0;
-        int phase = PREP;
-        const int spp = F.spp, maxB = F.max_bounce;
-
-        while (s < spp) {
-            if (phase == PREP) {
-                bool done = true;
-                if (j > maxB) {
-                    // loop of naiveGI never entered (maxBounce < 0): sample stays 1
-                } else if (!hit) {
-                    so = rtm_scale(rtm_mul(so, sample_ibl<COUNT>(S, Rd, c)), e4);
-                } else {
-                    const Mat cm = load_mat(S.mat, mid);
-                    if (cm.type == 0) {
-                        so = rtm_scale(so, cm.rough);
-                    } else {
-                        float invPdf = 0.0f;
-                        rtm_f3 brdf = rtm_v3(0, 0, 0);
-                        if (cm.type == 1) {
-                            Bd = hemi_cosine(n, &seed1, &seed0, &invPdf);
-                            brdf = rtm_scale(cm.color, 1.0f / 3.14f);
-                        } else if (cm.type == 2) {
-                            Bd = hemi_uniform(n, &seed1, &seed0, &invPdf);
-                            brdf = brdf_ggx(cm.color, cm.rough, rtm_scale(Rd, -1.0f), Bd, n);
-                        } else {
-                            Bd = Rd;
-                            brdf = cm.color;
-                            invPdf = 1.0f / rtm_fabs(rtm_dot(Bd, rtm_normalize(n)));
-                        }
-                        const rtm_f3 nd = rtm_normalize(Rd);
-                        Bo = rtm_v3(fmaf(nd.x, k, Ro.x), fmaf(nd.y, k, Ro.y), fmaf(nd.z, k, Ro.z));
-                        // attenuation only depends on pre-trace values: apply now
-                        const float att = invPdf * rtm_fabs(rtm_dot(Bd, rtm_normalize(n)));
-                        so = rtm_scale(rtm_mul(so, brdf), att);
-                        phase = BOUNCE;
-                        done = false;
-                    }
-                }
-                if (done) {
-                    if (LOG && logme) log_event(F, 3.0f, s + 1, rtm_v3(0, 0, 0), rtm_v3(0, 0, 0), 0.0f, 0, so);
-                    acc = rtm_add(acc, so);
-                    ++s;
-                    Ro = co; Rd = cd; n = nc; hit = hitc; k = hc.k; mid = mc; j = 0;
-                    so = rtm_v3(1, 1, 1);
-                    continue;
-                }
-            }
-            // one ray per lane per iteration
-            const rtm_f3 td = (phase == BOUNCE) ? Bd : sun;
-            const Hit h = trace<TRAV, COUNT>(S, Bo, td, stk, B, c);
-            bool finish = false;
-            if (LOG && logme) {
-                const int hm = h.tri >= 0 ? __float_as_int(S.tri_shade[h.tri].w) : 0;
-                log_event(F, phase == BOUNCE ? 1.0f : 2.0f, j, Bo, td, h.tri >= 0 ? h.k : -1.0f, hm, so);
-            }
-            if (phase == BOUNCE) {
-                if (h.tri >= 0) {
-                    const float4 sh = S.tri_shade[h.tri];
-                    Ro = Bo; Rd = Bd; hit = true; k = h.k; n = xyz(sh); mid = __float_as_int(sh.w);
-                    const Mat bm = load_mat(S.mat, mid);
-                    if (bm.type != 0) {
-                        if (j == maxB) {
-                            so = rtm_v3(0, 0, 0);
-                            finish = true;
-                        } else {
-                            ++j;
-                            phase = PREP;
-                        }
-                    } else {
-                        so = rtm_scale(so, bm.rough);
-                        finish = true;
-                    }
-                } else {
-                    phase = SUN;
-                }
+        if (phase == PREP) {
+            // naiveGI loop head for bounce j (Raytracing.cl:46-79); may complete samples without tracing
+            bool done = true;
+            if (j > maxB) {
+                // naiveGI's loop never entered (maxBounce < 0): the sample stays 1
+            } else if (tri < 0) {
+                so = rtm_scale(rtm_mul(so, sample_ibl<COUNT>(S, C, Rd, c)), e4);
             } else {
-                rtm_f3 sunLight = rtm_v3(0, 0, 0);
-                const Mat cm = load_mat(S.mat, mid);
-                if (h.tri < 0 && cm.type != 3) sunLight = rtm_v3(e3, e3, e3);
-                if (h.tri >= 0) {
-                    const float4 sh = S.tri_shade[h.tri];
-                    const Mat sm = load_mat(S.mat, __float_as_int(sh.w));
-                    if (sm.type == 3) sunLight = rtm_scale(sm.color, e3);
+                const float4 sh = S.tri_shade[tri];
+                const rtm_f3 n = xyz(sh);
+                const Mat cm = load_mat(S.mat, __float_as_int(sh.w));
+                if (cm.type == 0) {
+                    so = rtm_scale(so, cm.rough);
+                } else {
+                    const float4 f2 = S.tri_frame[3 * tri + 2];
+                    const rtm_f3 nn = xyz(f2);
+                    float invPdf = 0.0f;
+                    rtm_f3 brdf = rtm_v3(0, 0, 0);
+                    if (cm.type == 1) {
+                        Bd = hemi_cosine(n, S.tri_frame[3 * tri], S.tri_frame[3 * tri + 1], f2, &seed1, &seed0,
+                                         &invPdf);
+                        brdf = rtm_scale(cm.color, 1.0f / 3.14f);
+                    } else if (cm.type == 2) {
+                        Bd = hemi_uniform(n, S.tri_frame[3 * tri], S.tri_frame[3 * tri + 1], f2, &seed1, &seed0,
+                                          &invPdf);
+                        brdf = brdf_ggx(cm.color, cm.rough, rtm_scale(Rd, -1.0f), Bd, n);
+                    } else {
+                        Bd = Rd;
+                        brdf = cm.color;
+                        invPdf = 1.0f / rtm_fabs(rtm_dot(Bd, nn));
+                    }
+                    const rtm_f3 nd = rtm_normalize(Rd);
+                    Bo = rtm_v3(fmaf(nd.x, k, Ro.x), fmaf(nd.y, k, Ro.y), fmaf(nd.z, k, Ro.z));
+                    // attenuation depends only on pre-trace values (Raytracing.cl:86-87): apply now
+                    const float att = invPdf * rtm_fabs(rtm_dot(Bd, nn));
+                    so = rtm_scale(rtm_mul(so, brdf), att);
+                    phase = BOUNCE;
+                    done = false;
                 }
-                const rtm_f3 envLight = rtm_scale(sample_ibl<COUNT>(S, Bd, c), e4);
-                so = rtm_mul(so, rtm_add(sunLight, envLight));
-                finish = true;
             }
-            if (finish) {
+            if (done) {
                 if (LOG && logme) log_event(F, 3.0f, s + 1, rtm_v3(0, 0, 0), rtm_v3(0, 0, 0), 0.0f, 0, so);
                 acc = rtm_add(acc, so);
                 ++s;
-                Ro = co; Rd = cd; n = nc; hit = hitc; k = hc.k; mid = mc; j = 0;
+                if (s >= spp) {
+                    phase = FETCH;
+                } else {
+                    Ro = C.position; Rd = cd; tri = tc; k = kc; j = 0;
+                    so = rtm_v3(1, 1, 1);
+                }
+                if (phase == FETCH) {
+                    const rtm_f3 o = rtm_div(acc, (float)spp);
+                    float* dst = out + 3 * (int64_t)p;
+                    dst[0] = rtm_fmax(rtm_fmin(o.x, 1.0f), 0.0f);
+                    dst[1] = rtm_fmax(rtm_fmin(o.y, 1.0f), 0.0f);
+                    dst[2] = rtm_fmax(rtm_fmin(o.z, 1.0f), 0.0f);
+                }
+                continue;
+            }
+        }
+
+        // -- one ray per busy lane --
+        const rtm_f3 to = (phase == PRIMARY) ? C.position : Bo;
+        const rtm_f3 td = (phase == PRIMARY) ? cd : ((phase == BOUNCE) ? Bd : C.sun);
+        const Hit h = trace<TRAV, COUNT>(S, to, td, stk, B, c);
+        bool finish = false;
+        if (phase == PRIMARY) {
+            tc = h.tri;
+            kc = h.k;
+            Ro = C.position; Rd = cd; tri = tc; k = kc; j = 0;
+            so = rtm_v3(1, 1, 1);
+            phase = PREP;
+            if (spp <= 0) {   // reference: output = 0/0 -> NaN -> clamp gives 1
+                const rtm_f3 o = rtm_div(acc, (float)spp);
+                float* dst = out + 3 * (int64_t)p;
+                dst[0] = rtm_fmax(rtm_fmin(o.x, 1.0f), 0.0f);
+                dst[1] = rtm_fmax(rtm_fmin(o.y, 1.0f), 0.0f);
+                dst[2] = rtm_fmax(rtm_fmin(o.z, 1.0f), 0.0f);
+                phase = FETCH;
+            }
+            continue;
+        }
+        if (LOG && logme) {
+            const int hm = h.tri >= 0 ? __float_as_int(S.tri_shade[h.tri].w) : 0;
+            log_event(F, phase == BOUNCE ? 1.0f : 2.0f, j, Bo, td, h.tri >= 0 ? h.k : -1.0f, hm, so);
+        }
+        if (phase == BOUNCE) {
+            if (h.tri >= 0) {
+                Ro = Bo; Rd = Bd; tri = h.tri; k = h.k;
+                const Mat bm = load_mat(S.mat, __float_as_int(S.tri_shade[h.tri].w));
+                if (bm.type != 0) {
+                    if (j == maxB) {
+                        so = rtm_v3(0, 0, 0);
+                        finish = true;
+                    } else {
+                        ++j;
+                        phase = PREP;
+                    }
+                } else {
+                    so = rtm_scale(so, bm.rough);
+                    finish = true;
+                }
+            } else {
+                phase = SUN;
+            }
+        } else {  // SUN (Raytracing.cl:115-137)
+            rtm_f3 sunLight = rtm_v3(0, 0, 0);
+            const Mat cm = load_mat(S.mat, __float_as_int(S.tri_shade[tri].w));
+            if (h.tri < 0 && cm.type != 3) sunLight = rtm_v3(e3, e3, e3);
+            if (h.tri >= 0) {
+                const Mat sm = load_mat(S.mat, __float_as_int(S.tri_shade[h.tri].w));
+                if (sm.type == 3) sunLight = rtm_scale(sm.color, e3);
+            }
+            const rtm_f3 envLight = rtm_scale(sample_ibl<COUNT>(S, C, Bd, c), e4);
+            so = rtm_mul(so, rtm_add(sunLight, envLight));
+            finish = true;
+        }
+        if (finish) {
+            if (LOG && logme) log_event(F, 3.0f, s + 1, rtm_v3(0, 0, 0), rtm_v3(0, 0, 0), 0.0f, 0, so);
+            acc = rtm_add(acc, so);
+            ++s;
+            if (s >= spp) {
+                const rtm_f3 o = rtm_div(acc, (float)spp);
+                float* dst = out + 3 * (int64_t)p;
+                dst[0] = rtm_fmax(rtm_fmin(o.x, 1.0f), 0.0f);
+                dst[1] = rtm_fmax(rtm_fmin(o.y, 1.0f), 0.0f);
+                dst[2] = rtm_fmax(rtm_fmin(o.z, 1.0f), 0.0f);
+                phase = FETCH;
+            } else {
+                Ro = C.position; Rd = cd; tri = tc; k = kc; j = 0;
                 so = rtm_v3(1, 1, 1);
                 phase = PREP;
             }
         }
-        const rtm_f3 o = rtm_div(acc, (float)spp);
-        float* dst = out + 3 * p;
-        dst[0] = rtm_fmax(rtm_fmin(o.x, 1.0f), 0.0f);
-        dst[1] = rtm_fmax(rtm_fmin(o.y, 1.0f), 0.0f);
-        dst[2] = rtm_fmax(rtm_fmin(o.z, 1.0f), 0.0f);
     }
     if (COUNT) {
         unsigned long long v[5] = {c.nodes, c.tris, c.rays, c.env, c.dropped};
@@ -498,7 +657,7 @@ __global__ void __launch_bounds__(256) render_kernel(DevScene S, FrameParams F, 
         for (int q = 0; q < 5; ++q) {
             unsigned long long x = v[q];
             for (int off = 32; off > 0; off >>= 1) x += __shfl_down(x, off, 64);
-            if ((threadIdx.x & 63) == 0 && x) atomicAdd(&counts[q], x);
+            if (lane == 0 && x) atomicAdd(&counts[q], x);
         }
     }
 }
@@ -511,15 +670,30 @@ __global__ void gamma_kernel(const float* __restrict__ in, float* __restrict__ o
     }
 }
 
-template <int TRAV, bool COUNT>
+template <int TRAV, bool COUNT, bool LOG>
 hipError_t launch_t(const DevScene& sc, const FrameParams& fp, int block, float* d_out, unsigned long long* d_counts,
-                    hipStream_t stream) {
-    const int depth = (TRAV == TRAV_REF) ? REF_STACK : (sc.depth > 0 ? sc.depth : 1);
+                    unsigned int* d_work, hipStream_t stream) {
+    const int depth = (TRAV == TRAV_REF) ? REF_STACK : 2 * (sc.depth > 0 ? sc.depth : 1);  // FAST: int2 entries
     const size_t lds = (size_t)depth * block * sizeof(int);
-    const int64_t grid = (fp.nloc + block - 1) / block;
-    if (grid <= 0) return hipSuccess;
-    hipLaunchKernelGGL((render_kernel<TRAV, COUNT>), dim3((unsigned)grid), dim3(block), lds, stream, sc, fp, d_out,
-                       d_counts);
+    const int64_t need = (fp.nloc + block - 1) / block;
+    if (need <= 0) return hipSuccess;
+    // persistent grid: as many blocks as the device keeps resident (pixels are handed out by d_work)
+    int dev = 0, cus = 0, per_cu = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    if (e == hipSuccess)
+        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)render_kernel<TRAV, COUNT, LOG>, block,
+                                                         lds);
+    if (e != hipSuccess) return e;
+    const int64_t resident = (int64_t)std::max(1, cus) * std::max(1, per_cu);
+    const int64_t grid = std::min(need, resident);
+    e = hipMemsetAsync(d_work, 0, sizeof(unsigned int), stream);
+    if (e != hipSuccess) return e;
+    // the per-launch constants live after the counter in the same scratch block
+    LaunchConst* lc = reinterpret_cast<LaunchConst*>(reinterpret_cast<char*>(d_work) + 64);
+    hipLaunchKernelGGL(make_const_kernel, dim3(1), dim3(64), 0, stream, fp, lc);
+    hipLaunchKernelGGL((render_kernel<TRAV, COUNT, LOG>), dim3((unsigned)grid), dim3(block), lds, stream, sc, fp,
+                       d_out, d_counts, d_work, (const LaunchConst*)lc);
     return hipGetLastError();
 }
 
@@ -567,17 +741,15 @@ hipError_t launch_debug_math(int fn, const float* x, const float* y, float* out,
 }
 
 hipError_t launch_debug_log(const DevScene& sc, const FrameParams& fp, int traversal, float* d_out,
-                            hipStream_t stream) {
-    const int block = 64;
-    const int depth = traversal == TRAV_REF ? REF_STACK : (sc.depth > 0 ? sc.depth : 1);
-    const size_t lds = (size_t)depth * block * sizeof(int);
-    const int64_t grid = (fp.nloc + block - 1) / block;
-    if (traversal == TRAV_REF)
-        hipLaunchKernelGGL((render_kernel<TRAV_REF, false, true>), dim3((unsigned)grid), dim3(block), lds, stream, sc,
-                           fp, d_out, nullptr);
-    else
-        hipLaunchKernelGGL((render_kernel<TRAV_FAST, false, true>), dim3((unsigned)grid), dim3(block), lds, stream,
-                           sc, fp, d_out, nullptr);
+                            unsigned int* d_work, hipStream_t stream) {
+    if (traversal == TRAV_REF) return launch_t<TRAV_REF, false, true>(sc, fp, 64, d_out, nullptr, d_work, stream);
+    return launch_t<TRAV_FAST, false, true>(sc, fp, 64, d_out, nullptr, d_work, stream);
+}
+
+hipError_t launch_prep_frames(const DevScene& sc, float4* frame, hipStream_t stream) {
+    if (sc.ntri <= 0) return hipSuccess;
+    hipLaunchKernelGGL(prep_frames_kernel, dim3((unsigned)((sc.ntri + 255) / 256)), dim3(256), 0, stream, sc.tri_shade,
+                       sc.mat, sc.ntri, frame);
     return hipGetLastError();
 }
 
@@ -585,7 +757,7 @@ hipError_t launch_debug_trace(const DevScene& sc, int traversal, const float* ra
                               hipStream_t stream) {
     if (n <= 0) return hipSuccess;
     const int block = 128;
-    const int depth = traversal == TRAV_REF ? REF_STACK : (sc.depth > 0 ? sc.depth : 1);
+    const int depth = traversal == TRAV_REF ? REF_STACK : 2 * (sc.depth > 0 ? sc.depth : 1);
     const size_t lds = (size_t)depth * block * sizeof(int);
     if (traversal == TRAV_REF)
         hipLaunchKernelGGL(debug_trace_kernel<TRAV_REF>, dim3((unsigned)((n + block - 1) / block)), dim3(block), lds,
@@ -597,13 +769,13 @@ hipError_t launch_debug_trace(const DevScene& sc, int traversal, const float* ra
 }
 
 hipError_t launch_render(const DevScene& sc, const FrameParams& fp, int traversal, int block, float* d_out,
-                         unsigned long long* d_counts, hipStream_t stream) {
+                         unsigned long long* d_counts, unsigned int* d_work, hipStream_t stream) {
     if (traversal == TRAV_REF) {
-        return d_counts ? launch_t<TRAV_REF, true>(sc, fp, block, d_out, d_counts, stream)
-                        : launch_t<TRAV_REF, false>(sc, fp, block, d_out, d_counts, stream);
+        return d_counts ? launch_t<TRAV_REF, true, false>(sc, fp, block, d_out, d_counts, d_work, stream)
+                        : launch_t<TRAV_REF, false, false>(sc, fp, block, d_out, d_counts, d_work, stream);
     }
-    return d_counts ? launch_t<TRAV_FAST, true>(sc, fp, block, d_out, d_counts, stream)
-                    : launch_t<TRAV_FAST, false>(sc, fp, block, d_out, d_counts, stream);
+    return d_counts ? launch_t<TRAV_FAST, true, false>(sc, fp, block, d_out, d_counts, d_work, stream)
+                    : launch_t<TRAV_FAST, false, false>(sc, fp, block, d_out, d_counts, d_work, stream);
 }
 
 hipError_t launch_gamma(const float* d_in, float* d_out, int64_t n, hipStream_t stream) {

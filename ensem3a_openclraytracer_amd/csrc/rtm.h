@@ -49,6 +49,16 @@ RTM_FN float rtm_as_float(uint32_t u) { float f; __builtin_memcpy(&f, &u, 4); re
 RTM_FN float rtm_nan(void) { return rtm_as_float(0x7fc00000u); }
 RTM_FN float rtm_fabs(float x) { return rtm_as_float(rtm_as_uint(x) & 0x7fffffffu); }
 
+/* float -> int with one definition on every platform (C's cast is undefined
+ * outside the int range and the CPU and GPU disagree there): NaN -> 0,
+ * out-of-range values saturate. */
+RTM_FN int rtm_f2i(float x) {
+    if (!(x == x)) return 0;
+    if (x >= 2147483520.0f) return 2147483647;
+    if (x <= -2147483648.0f) return (-2147483647 - 1);
+    return (int)x;
+}
+
 /* IEEE-754 maxNum/minNum (a NaN operand yields the other one), with equal
  * operands -- including +0/-0 -- resolved to b so the sign of a zero result
  * never depends on the platform's min/max instruction. */
@@ -91,7 +101,7 @@ RTM_FN void rtm_sincos(float x, float* s_out, float* c_out) {
     float r = fmaf(-kf, RTM_PIO2_HI, x);
     r = fmaf(-kf, RTM_PIO2_LO, r);
     r = fmaf(-kf, RTM_PIO2_L2, r);
-    const int q = ((int)kf) & 3;
+    const int q = rtm_f2i(kf) & 3;
     const float z = r * r;
     const float ps = fmaf(fmaf(-1.9515295891e-4f, z, 8.3321608736e-3f), z, -1.6666654611e-1f);
     const float sn = fmaf(ps * z, r, r);
@@ -186,18 +196,32 @@ RTM_FN rtm_f4 rtm_qmul(rtm_f4 q, rtm_f4 p) {
     return rtm_v4(w, fmaf(qv.x, p.x, pv.x * q.x) + c.x, fmaf(qv.y, p.x, pv.y * q.x) + c.y,
                   fmaf(qv.z, p.x, pv.z * q.x) + c.z);
 }
-/* rotateVec(angle, axis, v) (MathLib.cl:56-65). */
-RTM_FN rtm_f3 rtm_rotate(float angle, rtm_f3 axis, rtm_f3 v) {
+/* rotateVec(angle, axis, v) (MathLib.cl:56-65), split in two so a rotation
+ * whose angle and axis are known ahead (camera, sun, IBL frame, the hemisphere
+ * frame of a triangle) is prepared once and applied many times with exactly
+ * the same arithmetic:
+ *   q    = (cos(angle/2), normalize(axis) * sin(angle/2))
+ *   qinv = normalize((q.x, -q.yzw) * (q.x^2 + |q.yzw|^2))
+ *   v'   = (q * (0, v) * qinv).yzw                                        */
+typedef struct { rtm_f4 q, qinv; } rtm_rot;
+RTM_FN rtm_rot rtm_rot_prepare(float angle, rtm_f3 axis) {
     float s, c;
     rtm_sincos(angle * 0.5f, &s, &c);
     const rtm_f3 an = rtm_normalize(axis);
-    const rtm_f4 q = rtm_v4(c, an.x * s, an.y * s, an.z * s);
+    rtm_rot r;
+    r.q = rtm_v4(c, an.x * s, an.y * s, an.z * s);
+    const float n2 = fmaf(r.q.x, r.q.x, rtm_dot(rtm_v3(r.q.y, r.q.z, r.q.w), rtm_v3(r.q.y, r.q.z, r.q.w)));
+    const rtm_f4 qc = rtm_v4(r.q.x * n2, (r.q.y * -1.0f) * n2, (r.q.z * -1.0f) * n2, (r.q.w * -1.0f) * n2);
+    r.qinv = rtm_normalize4(qc);
+    return r;
+}
+RTM_FN rtm_f3 rtm_rot_apply(rtm_rot r, rtm_f3 v) {
     const rtm_f4 V = rtm_v4(0.0f, v.x, v.y, v.z);
-    const float n2 = fmaf(q.x, q.x, rtm_dot(rtm_v3(q.y, q.z, q.w), rtm_v3(q.y, q.z, q.w)));
-    const rtm_f4 qc = rtm_v4(q.x * n2, (q.y * -1.0f) * n2, (q.z * -1.0f) * n2, (q.w * -1.0f) * n2);
-    const rtm_f4 qinv = rtm_normalize4(qc);
-    const rtm_f4 r = rtm_qmul(rtm_qmul(q, V), qinv);
-    return rtm_v3(r.y, r.z, r.w);
+    const rtm_f4 t = rtm_qmul(rtm_qmul(r.q, V), r.qinv);
+    return rtm_v3(t.y, t.z, t.w);
+}
+RTM_FN rtm_f3 rtm_rotate(float angle, rtm_f3 axis, rtm_f3 v) {
+    return rtm_rot_apply(rtm_rot_prepare(angle, axis), v);
 }
 
 /* ---- RNG (MathLib.cl:294-310) -------------------------------------------

@@ -80,7 +80,7 @@ int rt_render(rt_ctx* ctx, const float cam[10], const float env[5], int64_t npix
 /* Asynchronous render of the rows row0, row0+row_step, ... (row width
  * (int)cam[6], frame of npix pixels) on device device_index into DEVICE
  * memory d_out (packed: row k of the tile at d_out[3*W*k]), enqueued on the
- * HIP stream `stream` (NULL = the context's stream for that device).  Used
+ * HIP stream `stream` (a hipStream_t; NULL = the default stream).  Used
  * by the multi-process (one rank per GPU) path and the benchmark.  Returns
  * after the launch is enqueued. */
 int rt_render_device(rt_ctx* ctx, int device_index, const float cam[10], const float env[5],

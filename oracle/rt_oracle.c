@@ -108,7 +108,7 @@ static void SampleSphericalMap(float3 d, float* u, float* v) {
  * clamped to the edge (pinned by the GPU KAT). */
 static float3 ibl_fetch(const oracle_scene* sc, int x, int y) {
     const int W = sc->ibl_w, H = sc->ibl_h;
-    int x0 = x - 1, x1 = x, y0 = y - 1, y1 = y;
+    int x0 = x > -2147483647 ? x - 1 : x, x1 = x, y0 = y > -2147483647 ? y - 1 : y, y1 = y;
     x0 = x0 < 0 ? 0 : (x0 > W - 1 ? W - 1 : x0);
     x1 = x1 < 0 ? 0 : (x1 > W - 1 ? W - 1 : x1);
     y0 = y0 < 0 ? 0 : (y0 > H - 1 ? H - 1 : y0);
@@ -130,8 +130,8 @@ static float3 sampleIBL(const oracle_scene* sc, float3 dir, oracle_counts* cnt) 
     float u, v;
     SampleSphericalMap(dir, &u, &v);
     if (cnt) cnt->env++;
-    const int x = (int)(u * (float)sc->ibl_w);
-    const int y = (int)(v * (float)sc->ibl_h);
+    const int x = rtm_f2i(u * (float)sc->ibl_w);   /* (int2)(...) conversion; NaN/overflow pinned by rtm_f2i */
+    const int y = rtm_f2i(v * (float)sc->ibl_h);
     return rtm_scale(ibl_fetch(sc, x, y), 1.0f);
 }
 

@@ -94,10 +94,10 @@ def kat_inputs(rng):
     nn /= np.linalg.norm(nn, axis=1, keepdims=True)
     nn[:4] = [[0, 0, 1], [0, 0, -1], [0.0, 0.9626, 0.2708], [-0.9626, -0.2708, 0]]
     k["hemi_n"] = nn.astype(np.float32)
-    k["hemi_seeds"] = rng.integers(0, 2**32, size=(3000, 2), dtype=np.uint64).astype(np.uint32)
+    k["hemi_seeds_in"] = rng.integers(0, 2**32, size=(3000, 2), dtype=np.uint64).astype(np.uint32)
     # elementary functions
-    k["math_x"] = np.concatenate([rng.uniform(-10, 10, 20000), rng.uniform(-1, 1, 20000)]).astype(np.float32)
-    k["math_y"] = rng.uniform(-10, 10, 40000).astype(np.float32)
+    k["math_x"] = np.concatenate([rng.uniform(-10, 10, 4000), rng.uniform(-1, 1, 4000)]).astype(np.float32)
+    k["math_y"] = rng.uniform(-10, 10, 8000).astype(np.float32)
     return k
 
 
@@ -146,7 +146,7 @@ def main(outdir):
         res["ibl_small_out"] = refcl.kat_ibl(k["small_ibl"], k["ibl_dirs"])
         res["texel_out"] = refcl.kat_texel(k["small_ibl"], k["texel_xy"])
     for kind in (1, 2):
-        d, s = refcl.kat_hemi(kind, k["hemi_n"], k["hemi_seeds"])
+        d, s = refcl.kat_hemi(kind, k["hemi_n"], k["hemi_seeds_in"].copy())
         res[f"hemi{kind}_out"], res[f"hemi{kind}_state"] = d, s
     for fn in range(8):
         res[f"math{fn}_out"] = refcl.kat_math(fn, k["math_x"], k["math_y"])
