@@ -33,6 +33,11 @@ namespace rt {
 
 namespace {
 
+// Scenes whose BVH2 nodes + triangles take at most this many bytes are staged in LDS.
+#ifndef RT_LDS_SCENE_MAX
+#define RT_LDS_SCENE_MAX (24 * 1024)
+#endif
+
 constexpr int TRAV_FAST = 0;
 constexpr int TRAV_REF = 1;
 constexpr int REF_STACK = 20;  // stack.cl:4, Raytracing capacity 20
@@ -175,7 +180,8 @@ __device__ __forceinline__ bool mt_flat(const float4* __restrict__ tg, int t, rt
 // (one triangle test).  Popped items whose entry distance is beyond the best hit
 // are discarded without a fetch.  Stack entries: int2 (ref, tmin bits) in LDS.
 template <bool COUNT>
-__device__ Hit trace_fast(const DevScene& S, rtm_f3 o, rtm_f3 d, int* __restrict__ stk_base, int B, Cnt& c) {
+__device__ Hit trace_fast(const DevScene& S, const float4* __restrict__ nodes, const float4* __restrict__ tris,
+                          rtm_f3 o, rtm_f3 d, int* __restrict__ stk_base, int B, Cnt& c) {
     Hit best{1000.0f, -1};
     int best_rank = -1;
     if (COUNT) c.rays++;
@@ -189,7 +195,6 @@ __device__ Hit trace_fast(const DevScene& S, rtm_f3 o, rtm_f3 d, int* __restrict
     if (!(tmax >= tmin && tmax >= 0.0f)) return best;
     int item = S.root_ref;
     int sp = 0;
-    const float4* __restrict__ nodes = S.nodes;
     while (true) {
         if (item >= 0) {
             if (COUNT) c.nodes++;
@@ -220,7 +225,7 @@ __device__ Hit trace_fast(const DevScene& S, rtm_f3 o, rtm_f3 d, int* __restrict
             float k;
             int rank;
             const int t = ~item;
-            if (mt_flat(S.tri_geo, t, o, d, &k, &rank) && k > 0.0001f &&
+            if (mt_flat(tris, t, o, d, &k, &rank) && k > 0.0001f &&
                 (k < best.k || (k == best.k && rank < best_rank))) {
                 best.k = k;
                 best.tri = t;
@@ -243,9 +248,10 @@ __device__ Hit trace_fast(const DevScene& S, rtm_f3 o, rtm_f3 d, int* __restrict
 }
 
 template <int TRAV, bool COUNT>
-__device__ __forceinline__ Hit trace(const DevScene& S, rtm_f3 o, rtm_f3 d, int* stk, int B, Cnt& c) {
+__device__ __forceinline__ Hit trace(const DevScene& S, const float4* nodes, const float4* tris, rtm_f3 o, rtm_f3 d,
+                                     int* stk, int B, Cnt& c) {
     if (TRAV == TRAV_REF) return trace_ref<COUNT>(S, o, d, stk, B, c);
-    return trace_fast<COUNT>(S, o, d, stk, B, c);
+    return trace_fast<COUNT>(S, nodes, tris, o, d, stk, B, c);
 }
 
 // ---- per-launch constants (Raytracing.cl:18-37, 115-118; MathLib.cl:72-80) ----
@@ -443,22 +449,45 @@ __device__ __forceinline__ void log_event(const FrameParams& F, float kind, int 
 
 enum Phase { FETCH = 0, PRIMARY = 1, PREP = 2, BOUNCE = 3, SUN = 4, DONE = 5 };
 
+// RT_MIN_WAVES: waves per SIMD the register allocator must leave room for (0 = compiler's choice).
+#ifndef RT_MIN_WAVES
+#define RT_MIN_WAVES 0
+#endif
+#if RT_MIN_WAVES > 0
+#define RT_RENDER_BOUNDS __launch_bounds__(256, RT_MIN_WAVES)
+#else
+#define RT_RENDER_BOUNDS __launch_bounds__(256)
+#endif
+
 // One persistent lane = one pixel at a time.  Lanes that finish their pixel
 // take the next pixel index from a global counter: the wave ballots the lanes
 // that need work, one lane adds the count to the counter, and each lane takes
 // base + (its rank among the requesting lanes) -- so no lane idles while the
 // rest of its wave finishes a slower pixel.  Per loop iteration every busy
 // lane traces exactly one ray (primary, bounce or sun ray).
-template <int TRAV, bool COUNT, bool LOG = false>
-__global__ void __launch_bounds__(256) render_kernel(DevScene S, FrameParams F, float* __restrict__ out,
-                                                     unsigned long long* __restrict__ counts,
-                                                     unsigned int* __restrict__ work_counter,
-                                                     const LaunchConst* __restrict__ lconst) {
+template <int TRAV, bool COUNT, bool LOG = false, bool SMEM = false>
+__global__ void RT_RENDER_BOUNDS render_kernel(DevScene S, FrameParams F, float* __restrict__ out,
+                                               unsigned long long* __restrict__ counts,
+                                               unsigned int* __restrict__ work_counter,
+                                               const LaunchConst* __restrict__ lconst) {
     extern __shared__ int lds_stack[];
     const int B = blockDim.x;
     int* stk = lds_stack + threadIdx.x;
     Cnt c{0, 0, 0, 0, 0};
     const LaunchConst& C = *lconst;   // uniform: scalar loads, no VGPRs
+    // SMEM: the whole BVH2 node array and triangle array of a small scene are
+    // staged in LDS behind the stacks, once per (persistent) block.
+    const float4* nodes = S.nodes;
+    const float4* tris = S.tri_geo;
+    if (SMEM) {
+        float4* ln = reinterpret_cast<float4*>(lds_stack + 2 * S.depth * B);
+        float4* lt = ln + 4 * S.nnodes;
+        for (int q = threadIdx.x; q < 4 * S.nnodes; q += B) ln[q] = S.nodes[q];
+        for (int q = threadIdx.x; q < 3 * S.ntri; q += B) lt[q] = S.tri_geo[q];
+        __syncthreads();
+        nodes = ln;
+        tris = lt;
+    }
     const int W = F.width;
     const int imgSize = (int)F.npix;
     const float e3 = F.env[3], e4 = F.env[4];
@@ -580,7 +609,7 @@ __global__ void __launch_bounds__(256) render_kernel(DevScene S, FrameParams F, 
         // -- one ray per busy lane --
         const rtm_f3 to = (phase == PRIMARY) ? C.position : Bo;
         const rtm_f3 td = (phase == PRIMARY) ? cd : ((phase == BOUNCE) ? Bd : C.sun);
-        const Hit h = trace<TRAV, COUNT>(S, to, td, stk, B, c);
+        const Hit h = trace<TRAV, COUNT>(S, nodes, tris, to, td, stk, B, c);
         bool finish = false;
         if (phase == PRIMARY) {
             tc = h.tri;
@@ -670,11 +699,12 @@ __global__ void gamma_kernel(const float* __restrict__ in, float* __restrict__ o
     }
 }
 
-template <int TRAV, bool COUNT, bool LOG>
+template <int TRAV, bool COUNT, bool LOG, bool SMEM = false>
 hipError_t launch_t(const DevScene& sc, const FrameParams& fp, int block, float* d_out, unsigned long long* d_counts,
                     unsigned int* d_work, hipStream_t stream) {
     const int depth = (TRAV == TRAV_REF) ? REF_STACK : 2 * (sc.depth > 0 ? sc.depth : 1);  // FAST: int2 entries
-    const size_t lds = (size_t)depth * block * sizeof(int);
+    size_t lds = (size_t)depth * block * sizeof(int);
+    if (SMEM) lds += (size_t)(4 * sc.nnodes + 3 * sc.ntri) * sizeof(float4);
     const int64_t need = (fp.nloc + block - 1) / block;
     if (need <= 0) return hipSuccess;
     // persistent grid: as many blocks as the device keeps resident (pixels are handed out by d_work)
@@ -682,8 +712,8 @@ hipError_t launch_t(const DevScene& sc, const FrameParams& fp, int block, float*
     hipError_t e = hipGetDevice(&dev);
     if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     if (e == hipSuccess)
-        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)render_kernel<TRAV, COUNT, LOG>, block,
-                                                         lds);
+        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)render_kernel<TRAV, COUNT, LOG, SMEM>,
+                                                         block, lds);
     if (e != hipSuccess) return e;
     const int64_t resident = (int64_t)std::max(1, cus) * std::max(1, per_cu);
     const int64_t grid = std::min(need, resident);
@@ -692,8 +722,8 @@ hipError_t launch_t(const DevScene& sc, const FrameParams& fp, int block, float*
     // the per-launch constants live after the counter in the same scratch block
     LaunchConst* lc = reinterpret_cast<LaunchConst*>(reinterpret_cast<char*>(d_work) + 64);
     hipLaunchKernelGGL(make_const_kernel, dim3(1), dim3(64), 0, stream, fp, lc);
-    hipLaunchKernelGGL((render_kernel<TRAV, COUNT, LOG>), dim3((unsigned)grid), dim3(block), lds, stream, sc, fp,
-                       d_out, d_counts, d_work, (const LaunchConst*)lc);
+    hipLaunchKernelGGL((render_kernel<TRAV, COUNT, LOG, SMEM>), dim3((unsigned)grid), dim3(block), lds, stream, sc,
+                       fp, d_out, d_counts, d_work, (const LaunchConst*)lc);
     return hipGetLastError();
 }
 
@@ -726,7 +756,7 @@ __global__ void __launch_bounds__(256) debug_trace_kernel(DevScene S, const floa
     if (t >= n) return;
     Cnt c{0, 0, 0, 0, 0};
     const float* r = rays + 6 * t;
-    const Hit h = trace<TRAV, false>(S, rtm_v3(r[3], r[4], r[5]), rtm_v3(r[0], r[1], r[2]),
+    const Hit h = trace<TRAV, false>(S, S.nodes, S.tri_geo, rtm_v3(r[3], r[4], r[5]), rtm_v3(r[0], r[1], r[2]),
                                      lds_stack + threadIdx.x, blockDim.x, c);
     out[2 * t + 0] = h.k;
     out[2 * t + 1] = (float)h.tri;
@@ -773,6 +803,11 @@ hipError_t launch_render(const DevScene& sc, const FrameParams& fp, int traversa
     if (traversal == TRAV_REF) {
         return d_counts ? launch_t<TRAV_REF, true, false>(sc, fp, block, d_out, d_counts, d_work, stream)
                         : launch_t<TRAV_REF, false, false>(sc, fp, block, d_out, d_counts, d_work, stream);
+    }
+    const size_t scene_bytes = (size_t)(4 * sc.nnodes + 3 * sc.ntri) * sizeof(float4);
+    if (sc.ntri > 0 && scene_bytes <= (size_t)RT_LDS_SCENE_MAX) {
+        return d_counts ? launch_t<TRAV_FAST, true, false, true>(sc, fp, block, d_out, d_counts, d_work, stream)
+                        : launch_t<TRAV_FAST, false, false, true>(sc, fp, block, d_out, d_counts, d_work, stream);
     }
     return d_counts ? launch_t<TRAV_FAST, true, false>(sc, fp, block, d_out, d_counts, d_work, stream)
                     : launch_t<TRAV_FAST, false, false>(sc, fp, block, d_out, d_counts, d_work, stream);
