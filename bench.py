@@ -1,6 +1,6 @@
 """Benchmark of the path-tracing hot path (BASELINE.json metric).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config C2] [--traversal fast|ref]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config C2] [--traversal fast|ref] [--bvh sah|reference]
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
         --master-port P bench.py --gpus N --steps K --warmup W
 
@@ -65,18 +65,15 @@ def cpu_baseline(wl, scene, ibl, cam, env, target_s: float = 10.0):
     osc = O.OracleScene.from_scene(scene, ibl)
     W = int(cam[6])
     H = (wl.npix + W - 1) // W
-    # probe: one row in 64, to size the sample for ~target_s
+    # grow the row sample (rows 0::step) until it takes about target_s, or is the whole frame
     step = 64
-    t0 = time.perf_counter()
-    O.render(osc, cam, env, wl.npix, wl.spp, wl.max_bounce, row0=1, row_step=step, nthreads=threads)
-    probe = time.perf_counter() - t0
-    rows_probe = (H - 1 + step - 1) // step
-    per_row = probe / max(1, rows_probe)
-    want_rows = max(rows_probe, min(H, int(target_s / max(per_row, 1e-9))))
-    step = max(1, H // want_rows)
-    t0 = time.perf_counter()
-    O.render(osc, cam, env, wl.npix, wl.spp, wl.max_bounce, row0=0, row_step=step, nthreads=threads)
-    dt = time.perf_counter() - t0
+    while True:
+        t0 = time.perf_counter()
+        O.render(osc, cam, env, wl.npix, wl.spp, wl.max_bounce, row0=0, row_step=step, nthreads=threads)
+        dt = time.perf_counter() - t0
+        if dt >= 0.5 * target_s or step == 1:
+            break
+        step = max(1, min(step // 2, int(step * dt / target_s)))
     rows = (H + step - 1) // step
     samples = rows * W * wl.spp
     return {"value": samples / dt / 1e6, "unit": "Msamples/s", "cores": threads, "kind": "port",
@@ -91,6 +88,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="C2")
     ap.add_argument("--traversal", default="fast", choices=["fast", "ref"])
+    ap.add_argument("--bvh", default="sah", choices=["sah", "reference"])
     ap.add_argument("--block", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
@@ -113,6 +111,7 @@ def main():
     scene, cam, env, npix, spp, mb, ibl = wl.inputs()
     ctx = _native.Context(device_ids=[local])
     ctx.set_option("traversal", _native.RT_TRAVERSAL_FAST if args.traversal == "fast" else _native.RT_TRAVERSAL_REF)
+    ctx.set_option("bvh", _native.RT_BVH_SAH if args.bvh == "sah" else _native.RT_BVH_REFERENCE)
     if args.block:
         ctx.set_option("block", args.block)
     ctx.set_scene(scene.V_p, scene.V_n, scene.V_uv, scene.faceData, scene.materialData, scene.BVH.exportArray)
@@ -176,15 +175,27 @@ def main():
             "metric": METRIC, "value": round(value, 3), "unit": "Msamples/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4),
             "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f32",
-            "data": "reference bundled scene (ObjFiles/Cornell box.obj + .ini), resident in HBM",
+            "data": wl.data_note(),
             "config": {"workload": wl.name, "scene": wl.scene, "width": wl.width, "height": wl.height,
-                       "spp": spp, "max_bounce": mb, "traversal": args.traversal,
+                       "spp": spp, "max_bounce": mb, "traversal": args.traversal, "bvh": args.bvh,
                        "parallelism": f"row-interleaved x{world}" + (" + RCCL gather" if world > 1 else "")},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": _pmc_traffic(wl.name),
                          "kernel_ms": round(kernel_ms, 4), "alg_bytes_per_launch": int(alg_bytes),
                          "counts_per_sample": {k: round(v / (samples / world), 4) for k, v in cnt.items()}},
         }
+        if world == 1:
+            # the drop-in boundary's own rate: blocking rt_render into host memory (kernel + PCIe read-back)
+            host = np.zeros(3 * npix, np.float32)
+            ctx.render(cam, env, npix, spp, mb, out=host)
+            t0 = time.perf_counter()
+            for _ in range(3):
+                ctx.render(cam, env, npix, spp, mb, out=host)
+            dt = (time.perf_counter() - t0) / 3
+            line["host_boundary"] = {"value": round(samples / dt / 1e6, 3), "unit": "Msamples/s",
+                                     "ms_per_frame": round(dt * 1e3, 3),
+                                     "what": "rt_render (launch_Raytracing's C-ABI): kernel + device-to-host copy "
+                                             "of the frame into caller memory, scene already uploaded"}
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(wl, scene, ibl, cam, env)
         print(json.dumps(line), flush=True)

@@ -50,11 +50,13 @@ class KernelLauncher(object):
     and are not used (there is no OpenCL context).  ``device`` selects the
     GPU(s): ``None`` = device 0, an ``int`` = that device, a sequence of ints =
     render on all of them (rows interleaved).  Keyword ``traversal`` picks the
-    BVH traversal: ``"fast"`` (default) or ``"ref"`` (the reference's own DFS).
+    BVH traversal: ``"fast"`` (default) or ``"ref"`` (the reference's own DFS);
+    ``bvh`` the tree the fast traversal walks: ``"sah"`` (default) or
+    ``"reference"`` (the exported BVH.py tree) -- both give identical hits.
     """
 
     def __init__(self, context=None, platform=None, device: Union[None, int, Sequence[int]] = None, queue=None,
-                 traversal: str = "fast"):
+                 traversal: str = "fast", bvh: str = "sah"):
         self.platform = platform
         self.device = device
         self.context = context
@@ -67,6 +69,7 @@ class KernelLauncher(object):
             ids = list(device)
         self._ctx = _native.Context(device_ids=ids)
         self.set_traversal(traversal)
+        self.set_bvh(bvh)
         self._scene_key: Optional[tuple] = None
         self._env_key: Optional[tuple] = None
 
@@ -76,6 +79,13 @@ class KernelLauncher(object):
             raise ValueError("traversal must be 'fast' or 'ref'")
         self._ctx.set_option("traversal", mode)
         self.traversal = traversal
+
+    def set_bvh(self, bvh: str) -> None:
+        mode = {"reference": _native.RT_BVH_REFERENCE, "sah": _native.RT_BVH_SAH}.get(bvh)
+        if mode is None:
+            raise ValueError("bvh must be 'sah' or 'reference'")
+        self._ctx.set_option("bvh", mode)
+        self.bvh = bvh
 
     @property
     def native(self) -> _native.Context:

@@ -18,12 +18,15 @@ _lib = None
 
 RT_TRAVERSAL_FAST = 0
 RT_TRAVERSAL_REF = 1
+RT_BVH_REFERENCE = 0
+RT_BVH_SAH = 1
 
 # Every symbol of include/rt_api.h and include/rt_debug.h (checked by tests).
 EXPORTED = (
     "rt_create", "rt_destroy", "rt_last_error", "rt_set_scene", "rt_set_env", "rt_set_option",
     "rt_render", "rt_render_device", "rt_tile_rows", "rt_count_work", "rt_work_bytes", "rt_gamma",
     "rt_bvh_build", "rt_device_count", "rt_debug_math", "rt_debug_trace", "rt_debug_scene_info", "rt_debug_pixel_log",
+    "rt_debug_wave_counts",
 )
 
 _c_p = ctypes.c_void_p
@@ -78,6 +81,7 @@ def lib():
             "rt_debug_math": (_i32, [_c_p, _i32, _c_p, _c_p, _c_p, _i64]),
             "rt_debug_trace": (_i32, [_c_p, _i32, _c_p, _c_p, _i64]),
             "rt_debug_scene_info": (_i32, [_c_p, _c_p]),
+            "rt_debug_wave_counts": (_i32, [_c_p, _c_p, _c_p, _i64, _i32, _i32, _c_p]),
             "rt_debug_pixel_log": (_i32, [_c_p, _i32, _c_p, _c_p, _i64, _i32, _i32, _i64, _c_p, _i32, _c_p, _c_p]),
         }
         for name, (res, args) in sig.items():
@@ -218,6 +222,16 @@ class Context:
                                              int(max_bounce), int(pixel), log.ctypes.data, cap, ctypes.byref(n),
                                              out3.ctypes.data))
         return log[: n.value].copy(), out3
+
+    def wave_counts(self, cam, env, npix, spp, max_bounce):
+        """rt_debug_wave_counts: lane counters + wave-level loop iterations of one frame."""
+        c, e = f32(cam), f32(env)
+        out = np.zeros(7, dtype=np.uint64)
+        self._check(lib().rt_debug_wave_counts(self.handle, ptr(c), ptr(e), int(npix), int(spp), int(max_bounce),
+                                               out.ctypes.data))
+        keys = ("node_fetches", "tri_tests", "rays", "env_lookups", "stack_drops", "wave_trav_iters",
+                "wave_render_iters")
+        return {k: int(v) for k, v in zip(keys, out)}
 
     def scene_info(self):
         out = np.zeros(4, dtype=np.int64)

@@ -20,6 +20,7 @@
 
 #include "../../include/rt_api.h"
 #include "../../include/rt_debug.h"
+#include "bvh_sah.h"
 #include "rt_internal.h"
 
 namespace {
@@ -60,6 +61,7 @@ struct rt_ctx {
     bool have_env = false;
     int ibl_w = 0, ibl_h = 0;
     int traversal = RT_TRAVERSAL_FAST;
+    int bvh_layout = RT_BVH_SAH;
     int block = 128;
     std::string err;
 };
@@ -125,10 +127,57 @@ inline bool fidx(float v, int64_t limit, int32_t* out) {
     return true;
 }
 
+// Emit the FAST node array from a binary tree with one triangle per leaf:
+// internal nodes in BFS order, each holding both child boxes and refs.
+// box: 6 floats per tree node (lo.xyz, hi.xyz).
+void emit_bvh2(HostScene& hs, const int32_t* L, const int32_t* R, const int32_t* T, const float* box, int64_t nn) {
+    auto is_inner = [&](int64_t i) { return L[i] >= 0; };
+    std::vector<int32_t> wide_of(nn, -1), depth_of(nn, 0), bfs;
+    bfs.reserve(nn);
+    int32_t max_depth = 1;
+    if (is_inner(0)) {
+        bfs.push_back(0);
+        wide_of[0] = 0;
+    }
+    for (size_t h = 0; h < bfs.size(); ++h) {
+        const int32_t n = bfs[h];
+        for (int32_t ch : {L[n], R[n]}) {
+            if (!is_inner(ch)) continue;
+            wide_of[ch] = (int32_t)bfs.size();
+            depth_of[ch] = depth_of[n] + 1;
+            max_depth = std::max(max_depth, depth_of[ch] + 1);
+            bfs.push_back(ch);
+        }
+    }
+    hs.nnodes = (int32_t)bfs.size();
+    hs.nodes.assign((size_t)hs.nnodes * 16, 0.0f);
+    for (size_t w = 0; w < bfs.size(); ++w) {
+        const int32_t n = bfs[w];
+        const float* c0 = box + 6 * (int64_t)L[n];
+        const float* c1 = box + 6 * (int64_t)R[n];
+        float* o = hs.nodes.data() + 16 * w;
+        o[0] = c0[0]; o[1] = c0[3]; o[2] = c0[1]; o[3] = c0[4];
+        o[4] = c1[0]; o[5] = c1[3]; o[6] = c1[1]; o[7] = c1[4];
+        o[8] = c0[2]; o[9] = c0[5]; o[10] = c1[2]; o[11] = c1[5];
+        const int32_t r0 = is_inner(L[n]) ? wide_of[L[n]] : ~T[L[n]];
+        const int32_t r1 = is_inner(R[n]) ? wide_of[R[n]] : ~T[R[n]];
+        o[12] = as_f32(r0); o[13] = as_f32(r1); o[14] = 0.0f; o[15] = 0.0f;
+    }
+    hs.root_ref = is_inner(0) ? 0 : ~T[0];
+    for (int k = 0; k < 6; ++k) hs.root_box[k] = box[k];
+    hs.depth = max_depth;
+}
+
 // Pack the FAST layout from the reference export.  Returns false (with
 // reason) if the export is not a proper binary tree with one triangle per
-// leaf, in which case only the REF traversal is available.
-bool pack_fast(HostScene& hs, const float* bvh9, int64_t nn, int64_t ntri, std::string& why) {
+// leaf, in which case only the REF traversal is available.  layout
+// RT_BVH_REFERENCE keeps the reference's tree, RT_BVH_SAH regroups its leaf
+// boxes (bvh_sah.cpp); both give the same hits.
+bool pack_fast(HostScene& hs, const float* bvh9, int64_t nn, int64_t ntri, int layout, std::string& why) {
+    if (nn <= 0) {
+        why = "empty BVH";
+        return false;
+    }
     std::vector<int32_t> L(nn), R(nn), T(nn);
     for (int64_t i = 0; i < nn; ++i) {
         if (!fidx(bvh9[9 * i + 0], nn, &L[i]) || !fidx(bvh9[9 * i + 1], nn, &R[i]) ||
@@ -137,51 +186,40 @@ bool pack_fast(HostScene& hs, const float* bvh9, int64_t nn, int64_t ntri, std::
             return false;
         }
     }
-    // Classify reachable nodes, check the tree shape.
+    // Check the tree shape over the reachable nodes.
     std::vector<uint8_t> seen(nn, 0);
-    std::vector<int32_t> wide_of(nn, -1);
-    std::vector<int32_t> bfs;
-    bfs.reserve(nn);
     auto is_leaf = [&](int64_t i) { return L[i] == -1 && R[i] == -1 && T[i] >= 0; };
     auto is_inner = [&](int64_t i) { return L[i] >= 0 && R[i] >= 0 && T[i] == -1; };
     if (!is_leaf(0) && !is_inner(0)) {
         why = "root is neither a one-triangle leaf nor a two-child node";
         return false;
     }
-    std::vector<int32_t> tri_seen(ntri, 0);
-    // BFS over internal nodes
+    std::vector<int32_t> tri_seen(ntri, 0), leaves;
+    std::vector<int32_t> queue{0};
     seen[0] = 1;
-    if (is_inner(0)) {
-        bfs.push_back(0);
-        wide_of[0] = 0;
-    }
-    std::vector<int32_t> depth_of(nn, 0);
-    int32_t max_depth = 1;
-    for (size_t h = 0; h < bfs.size(); ++h) {
-        const int32_t n = bfs[h];
+    for (size_t h = 0; h < queue.size(); ++h) {
+        const int32_t n = queue[h];
+        if (is_leaf(n)) {
+            if (tri_seen[T[n]]++) {
+                why = "triangle in two leaves";
+                return false;
+            }
+            leaves.push_back(n);
+            continue;
+        }
+        if (!is_inner(n)) {
+            why = "node with one child, or with both a triangle and children";
+            return false;
+        }
         for (int32_t ch : {L[n], R[n]}) {
             if (seen[ch]) {
                 why = "node reachable twice (not a tree)";
                 return false;
             }
             seen[ch] = 1;
-            if (is_inner(ch)) {
-                wide_of[ch] = (int32_t)bfs.size();
-                depth_of[ch] = depth_of[n] + 1;
-                if (depth_of[ch] + 1 > max_depth) max_depth = depth_of[ch] + 1;
-                bfs.push_back(ch);
-            } else if (is_leaf(ch)) {
-                if (tri_seen[T[ch]]++) {
-                    why = "triangle in two leaves";
-                    return false;
-                }
-            } else {
-                why = "node with one child, or with both a triangle and children";
-                return false;
-            }
+            queue.push_back(ch);
         }
     }
-    if (is_leaf(0)) tri_seen[T[0]]++;
     // Rank of each leaf triangle in the reference visiting order: pre-order
     // DFS, right child first (push left then right, MathLib.cl:269-276).
     std::vector<int32_t> rank(ntri, 0x7fffffff);
@@ -197,25 +235,36 @@ bool pack_fast(HostScene& hs, const float* bvh9, int64_t nn, int64_t ntri, std::
             if (R[n] >= 0) st.push_back(R[n]);
         }
     }
-    hs.nnodes = (int32_t)bfs.size();
-    hs.nodes.assign((size_t)hs.nnodes * 16, 0.0f);
-    for (size_t w = 0; w < bfs.size(); ++w) {
-        const int32_t n = bfs[w];
-        const float* c0 = bvh9 + 9 * (int64_t)L[n];
-        const float* c1 = bvh9 + 9 * (int64_t)R[n];
-        float* o = hs.nodes.data() + 16 * w;
-        o[0] = c0[2]; o[1] = c0[5]; o[2] = c0[3]; o[3] = c0[6];
-        o[4] = c1[2]; o[5] = c1[5]; o[6] = c1[3]; o[7] = c1[6];
-        o[8] = c0[4]; o[9] = c0[7]; o[10] = c1[4]; o[11] = c1[7];
-        const int32_t r0 = is_inner(L[n]) ? wide_of[L[n]] : ~T[L[n]];
-        const int32_t r1 = is_inner(R[n]) ? wide_of[R[n]] : ~T[R[n]];
-        o[12] = as_f32(r0); o[13] = as_f32(r1); o[14] = 0.0f; o[15] = 0.0f;
-    }
-    hs.root_ref = is_inner(0) ? 0 : ~T[0];
-    for (int k = 0; k < 3; ++k) { hs.root_box[k] = bvh9[2 + k]; hs.root_box[3 + k] = bvh9[5 + k]; }
-    hs.depth = max_depth;
     for (int64_t t = 0; t < ntri; ++t) hs.tri_geo[12 * t + 3] = as_f32(rank[t]);
+    if (layout == RT_BVH_SAH && leaves.size() > 1) {
+        std::vector<float> lb(6 * leaves.size());
+        std::vector<int32_t> ids(leaves.size());
+        for (size_t q = 0; q < leaves.size(); ++q) {
+            const float* nd = bvh9 + 9 * (int64_t)leaves[q];
+            for (int k = 0; k < 6; ++k) lb[6 * q + k] = nd[2 + k];
+            ids[q] = T[leaves[q]];
+        }
+        rt::SahTree st;
+        rt::sah_build(lb.data(), ids.data(), (int64_t)leaves.size(), st);
+        emit_bvh2(hs, st.L.data(), st.R.data(), st.leaf.data(), st.box.data(), (int64_t)st.L.size());
+        return true;
+    }
+    std::vector<float> box(6 * nn);
+    for (int64_t i = 0; i < nn; ++i)
+        for (int k = 0; k < 6; ++k) box[6 * i + k] = bvh9[9 * i + 2 + k];
+    emit_bvh2(hs, L.data(), R.data(), T.data(), box.data(), nn);
     return true;
+}
+
+// pack_fast + the limits of the FAST kernels; sets hs.fast_ok.
+void pack_checked(HostScene& hs, const float* bvh9, int64_t nb, int64_t ntri, int layout, std::string& why) {
+    hs.fast_ok = (ntri > 0) ? pack_fast(hs, bvh9, nb, ntri, layout, why) : true;
+    if (ntri == 0) { hs.nnodes = 0; hs.root_ref = 0; hs.depth = 1; hs.nodes.clear(); }
+    if (hs.fast_ok && (int64_t)hs.depth * 256 * 8 > 64 * 1024) {  // int2 stack entries, block <= 256
+        hs.fast_ok = false;
+        why = "tree too deep for the LDS stack";
+    }
+    if (hs.nodes.empty()) hs.nodes.assign(16, 0.0f);
 }
 
 template <typename T>
@@ -340,6 +389,23 @@ int rt_set_option(rt_ctx* ctx, const char* key, int64_t value) {
         ctx->traversal = (int)value;
         return RT_OK;
     }
+    if (!std::strcmp(key, "bvh")) {
+        if (value != RT_BVH_REFERENCE && value != RT_BVH_SAH)
+            return set_err(ctx, RT_ERR_ARG, "bvh must be 0 (reference tree) or 1 (sah)");
+        ctx->bvh_layout = (int)value;
+        if (!ctx->have_scene) return RT_OK;
+        HostScene& hs = ctx->hs;   // repack the FAST nodes of the current scene
+        std::string why;
+        pack_checked(hs, hs.bvh9.data(), hs.nbvh9, hs.ntri, ctx->bvh_layout, why);
+        for (auto& d : ctx->devs) {
+            HIP_OR_RET(ctx, hipSetDevice(d.id));
+            HIP_OR_RET(ctx, upload(d.nodes, hs.nodes, d.stream));
+            HIP_OR_RET(ctx, upload(d.tri_geo, hs.tri_geo, d.stream));
+            HIP_OR_RET(ctx, hipStreamSynchronize(d.stream));
+        }
+        if (!hs.fast_ok) ctx->err = "FAST traversal unavailable (" + why + "); REF traversal will be used";
+        return RT_OK;
+    }
     if (!std::strcmp(key, "block")) {
         if (value != 64 && value != 128 && value != 256) return set_err(ctx, RT_ERR_ARG, "block must be 64/128/256");
         ctx->block = (int)value;
@@ -427,13 +493,7 @@ int rt_set_scene(rt_ctx* ctx, const float* vp, int64_t nvp, const float* vn, int
         }
     }
     std::string why;
-    hs.fast_ok = (T > 0) ? pack_fast(hs, bvh9, NB, T, why) : true;
-    if (T == 0) { hs.nnodes = 0; hs.root_ref = 0; hs.depth = 1; }
-    if (hs.fast_ok && (int64_t)hs.depth * 256 * 8 > 64 * 1024) {  // int2 stack entries, block <= 256
-        hs.fast_ok = false;
-        why = "tree too deep for the LDS stack";
-    }
-    if (hs.nodes.empty()) hs.nodes.assign(16, 0.0f);
+    pack_checked(hs, bvh9, NB, T, ctx->bvh_layout, why);
     for (auto& d : ctx->devs) {
         HIP_OR_RET(ctx, hipSetDevice(d.id));
         HIP_OR_RET(ctx, upload(d.nodes, hs.nodes, d.stream));
@@ -548,8 +608,9 @@ int rt_render(rt_ctx* ctx, const float cam[10], const float env[5], int64_t npix
     return RT_OK;
 }
 
-int rt_count_work(rt_ctx* ctx, const float cam[10], const float env[5], int64_t npix, int spp, int max_bounce,
-                  int row0, int row_step, uint64_t counts[5]) {
+namespace {
+int count_all(rt_ctx* ctx, const float cam[10], const float env[5], int64_t npix, int spp, int max_bounce, int row0,
+              int row_step, uint64_t* counts, int n) {
     rt::FrameParams fp;
     int st = check_frame(ctx, cam, env, npix, spp, row0, row_step, &fp);
     if (st) return st;
@@ -560,27 +621,37 @@ int rt_count_work(rt_ctx* ctx, const float cam[10], const float env[5], int64_t 
     HIP_OR_RET(ctx, hipSetDevice(d.id));
     const size_t bytes = (size_t)fp.nloc * 3 * sizeof(float);
     HIP_OR_RET(ctx, ensure(d.out, bytes > 0 ? bytes : 16));
-    HIP_OR_RET(ctx, ensure(d.counts, 5 * sizeof(unsigned long long)));
-    HIP_OR_RET(ctx, hipMemsetAsync(d.counts.p, 0, 5 * sizeof(unsigned long long), d.stream));
+    unsigned long long h[8] = {0};
+    HIP_OR_RET(ctx, ensure(d.counts, sizeof h));
+    HIP_OR_RET(ctx, hipMemsetAsync(d.counts.p, 0, sizeof h, d.stream));
     HIP_OR_RET(ctx, rt::launch_render(dev_scene(ctx, d), fp, effective_traversal(ctx), ctx->block, (float*)d.out.p,
                                       (unsigned long long*)d.counts.p, (unsigned int*)d.work.p, d.stream));
-    unsigned long long h[5];
     HIP_OR_RET(ctx, hipMemcpyAsync(h, d.counts.p, sizeof h, hipMemcpyDeviceToHost, d.stream));
     HIP_OR_RET(ctx, hipStreamSynchronize(d.stream));
-    for (int q = 0; q < 5; ++q) counts[q] = h[q];
+    for (int q = 0; q < n; ++q) counts[q] = h[q];
     return RT_OK;
+}
+}  // namespace
+
+int rt_count_work(rt_ctx* ctx, const float cam[10], const float env[5], int64_t npix, int spp, int max_bounce,
+                  int row0, int row_step, uint64_t counts[5]) {
+    return count_all(ctx, cam, env, npix, spp, max_bounce, row0, row_step, counts, 5);
+}
+
+int rt_debug_wave_counts(rt_ctx* ctx, const float cam[10], const float env[5], int64_t npix, int spp, int max_bounce,
+                         uint64_t counts[7]) {
+    return count_all(ctx, cam, env, npix, spp, max_bounce, 0, 1, counts, 7);
 }
 
 int rt_work_bytes(rt_ctx* ctx, double out[4]) {
+    // Algorithmic bytes per unit: 32 B per box test (24 B AABB + 8 B child/leaf
+    // refs), 36 B per triangle test (v0, e1, e2), 40 B per hit record, 16 B per IBL lookup.
     if (!ctx || !out) return set_err(ctx, RT_ERR_ARG, "null argument");
-    if (effective_traversal(ctx) == RT_TRAVERSAL_FAST) {
-        out[0] = 64.0;  // one BVH2 node: both child boxes + child refs (4 x float4)
-    } else {
-        out[0] = 36.0;  // one reference AoS node (9 floats)
-    }
-    out[1] = 48.0;  // one triangle test: a.p, e1, e2 (+ rank), 3 x float4
-    out[2] = 40.0;  // hit record: normal+material (16 B) + material row (24 B)
-    out[3] = 16.0;  // IBL lookup: 4 RGBA8 texels
+    out[0] = effective_traversal(ctx) == RT_TRAVERSAL_FAST ? 64.0   // one BVH2 node = both child boxes
+                                                            : 32.0;  // one reference node = one box
+    out[1] = 36.0;
+    out[2] = 40.0;
+    out[3] = 16.0;
     return RT_OK;
 }
 

@@ -49,7 +49,15 @@ struct Hit {
 
 struct Cnt {
     unsigned long long nodes, tris, rays, env, dropped;
+    unsigned long long wave_trav;   // traversal-loop iterations issued per wave (any lane active)
+    unsigned long long wave_outer;  // render-loop iterations per wave
 };
+constexpr int NCOUNTS = 7;
+
+// COUNT builds: the lowest active lane of the wave counts one wave-level iteration.
+__device__ __forceinline__ void count_wave(unsigned long long& x) {
+    if ((int)(threadIdx.x & 63) == __ffsll((long long)__ballot(1)) - 1) x++;
+}
 
 __device__ __forceinline__ rtm_f3 xyz(float4 v) { return rtm_v3(v.x, v.y, v.z); }
 
@@ -88,6 +96,7 @@ __device__ Hit trace_ref(const DevScene& S, rtm_f3 o, rtm_f3 d, int* __restrict_
     int top = 0;
     stk[0] = 0;
     while (top != -1) {
+        if (COUNT) count_wave(c.wave_trav);
         const int curr = stk[top * B];
         --top;
         if (COUNT) c.nodes++;
@@ -179,7 +188,7 @@ __device__ __forceinline__ bool mt_flat(const float4* __restrict__ tg, int t, rt
 // child continues, the farther is pushed with its entry distance) or a leaf
 // (one triangle test).  Popped items whose entry distance is beyond the best hit
 // are discarded without a fetch.  Stack entries: int2 (ref, tmin bits) in LDS.
-template <bool COUNT>
+template <bool COUNT, bool SOA>
 __device__ Hit trace_fast(const DevScene& S, const float4* __restrict__ nodes, const float4* __restrict__ tris,
                           rtm_f3 o, rtm_f3 d, int* __restrict__ stk_base, int B, Cnt& c) {
     Hit best{1000.0f, -1};
@@ -196,12 +205,17 @@ __device__ Hit trace_fast(const DevScene& S, const float4* __restrict__ nodes, c
     int item = S.root_ref;
     int sp = 0;
     while (true) {
+        if (COUNT) count_wave(c.wave_trav);
         if (item >= 0) {
             if (COUNT) c.nodes++;
-            const float4 a = nodes[4 * item + 0];
-            const float4 b = nodes[4 * item + 1];
-            const float4 z = nodes[4 * item + 2];
-            const float4 e = nodes[4 * item + 3];
+            // AoS: node i = nodes[4i .. 4i+3]; SOA (LDS copy): plane k at nodes[k * nnodes + i], so
+            // 16 lanes reading 16 different nodes hit 16 different bank groups
+            const float4* np = SOA ? nodes + item : nodes + 4 * item;
+            const int ks = SOA ? S.nnodes : 1;
+            const float4 a = np[0];
+            const float4 b = np[ks];
+            const float4 z = np[2 * ks];
+            const float4 e = np[3 * ks];
             float t0n, t0x, t1n, t1x;
             slab_fma(a.x, a.y, a.z, a.w, z.x, z.y, o.x, o.y, o.z, ix, iy, iz, oix, oiy, oiz, t0n, t0x);
             slab_fma(b.x, b.y, b.z, b.w, z.z, z.w, o.x, o.y, o.z, ix, iy, iz, oix, oiy, oiz, t1n, t1x);
@@ -247,11 +261,11 @@ __device__ Hit trace_fast(const DevScene& S, const float4* __restrict__ nodes, c
     return best;
 }
 
-template <int TRAV, bool COUNT>
+template <int TRAV, bool COUNT, bool SOA = false>
 __device__ __forceinline__ Hit trace(const DevScene& S, const float4* nodes, const float4* tris, rtm_f3 o, rtm_f3 d,
                                      int* stk, int B, Cnt& c) {
     if (TRAV == TRAV_REF) return trace_ref<COUNT>(S, o, d, stk, B, c);
-    return trace_fast<COUNT>(S, nodes, tris, o, d, stk, B, c);
+    return trace_fast<COUNT, SOA>(S, nodes, tris, o, d, stk, B, c);
 }
 
 // ---- per-launch constants (Raytracing.cl:18-37, 115-118; MathLib.cl:72-80) ----
@@ -473,7 +487,7 @@ __global__ void RT_RENDER_BOUNDS render_kernel(DevScene S, FrameParams F, float*
     extern __shared__ int lds_stack[];
     const int B = blockDim.x;
     int* stk = lds_stack + threadIdx.x;
-    Cnt c{0, 0, 0, 0, 0};
+    Cnt c{0, 0, 0, 0, 0, 0, 0};
     const LaunchConst& C = *lconst;   // uniform: scalar loads, no VGPRs
     // SMEM: the whole BVH2 node array and triangle array of a small scene are
     // staged in LDS behind the stacks, once per (persistent) block.
@@ -482,7 +496,7 @@ __global__ void RT_RENDER_BOUNDS render_kernel(DevScene S, FrameParams F, float*
     if (SMEM) {
         float4* ln = reinterpret_cast<float4*>(lds_stack + 2 * S.depth * B);
         float4* lt = ln + 4 * S.nnodes;
-        for (int q = threadIdx.x; q < 4 * S.nnodes; q += B) ln[q] = S.nodes[q];
+        for (int q = threadIdx.x; q < 4 * S.nnodes; q += B) ln[(q & 3) * S.nnodes + (q >> 2)] = S.nodes[q];
         for (int q = threadIdx.x; q < 3 * S.ntri; q += B) lt[q] = S.tri_geo[q];
         __syncthreads();
         nodes = ln;
@@ -543,6 +557,7 @@ __global__ void RT_RENDER_BOUNDS render_kernel(DevScene S, FrameParams F, float*
             }
         }
         if (__all(phase == DONE)) break;
+        if (COUNT && lane == 0) c.wave_outer++;
         if (phase == DONE) continue;
 
         if (phase == PREP) {
@@ -609,7 +624,7 @@ __global__ void RT_RENDER_BOUNDS render_kernel(DevScene S, FrameParams F, float*
         // -- one ray per busy lane --
         const rtm_f3 to = (phase == PRIMARY) ? C.position : Bo;
         const rtm_f3 td = (phase == PRIMARY) ? cd : ((phase == BOUNCE) ? Bd : C.sun);
-        const Hit h = trace<TRAV, COUNT>(S, nodes, tris, to, td, stk, B, c);
+        const Hit h = trace<TRAV, COUNT, SMEM>(S, nodes, tris, to, td, stk, B, c);
         bool finish = false;
         if (phase == PRIMARY) {
             tc = h.tri;
@@ -681,9 +696,9 @@ __global__ void RT_RENDER_BOUNDS render_kernel(DevScene S, FrameParams F, float*
         }
     }
     if (COUNT) {
-        unsigned long long v[5] = {c.nodes, c.tris, c.rays, c.env, c.dropped};
+        unsigned long long v[NCOUNTS] = {c.nodes, c.tris, c.rays, c.env, c.dropped, c.wave_trav, c.wave_outer};
 #pragma unroll
-        for (int q = 0; q < 5; ++q) {
+        for (int q = 0; q < NCOUNTS; ++q) {
             unsigned long long x = v[q];
             for (int off = 32; off > 0; off >>= 1) x += __shfl_down(x, off, 64);
             if (lane == 0 && x) atomicAdd(&counts[q], x);
@@ -754,7 +769,7 @@ __global__ void __launch_bounds__(256) debug_trace_kernel(DevScene S, const floa
     extern __shared__ int lds_stack[];
     const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= n) return;
-    Cnt c{0, 0, 0, 0, 0};
+    Cnt c{0, 0, 0, 0, 0, 0, 0};
     const float* r = rays + 6 * t;
     const Hit h = trace<TRAV, false>(S, S.nodes, S.tri_geo, rtm_v3(r[3], r[4], r[5]), rtm_v3(r[0], r[1], r[2]),
                                      lds_stack + threadIdx.x, blockDim.x, c);

@@ -97,6 +97,17 @@ class Workload:
         sc.params.update(self.params)
         return sc
 
+    def data_note(self) -> str:
+        src = {"cornell": "ObjFiles/Cornell box.obj + .ini", "monkey": "ObjFiles/Cornell box_Monkey.obj + .ini",
+               "serre": "ObjFiles/Serre_leger.obj + .ini", "proto": "ObjFiles/protoEnsem.obj + .ini",
+               "furnace": "ObjFiles/FurnaceHD.obj + .ini",
+               "grid1m": "synthetic 1M-triangle grid (SURVEY.md Appendix D)"}.get(self.scene, self.scene)
+        note = f"reference scene {src}" if self.scene != "grid1m" else src
+        if self.overrides:
+            note += " with the config's material overrides"
+        ibl = "8k IBL substitute (bilinear upscale of the bundled preview)" if self.ibl == "8k" else "bundled preview IBL"
+        return f"{note}, {ibl}; scene and IBL resident in HBM"
+
     def ibl_rgba(self) -> np.ndarray:
         return ibl_8k() if self.ibl == "8k" else ibl_preview()
 

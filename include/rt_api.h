@@ -42,6 +42,14 @@ enum rt_traversal {
     RT_TRAVERSAL_REF = 1   /* the reference's own DFS (MathLib.cl:234-288): no culling, 20-slot stack */
 };
 
+/* Tree the FAST traversal walks (rt_set_option "bvh").  Both trees hold the
+ * reference's leaf boxes bit for bit and give identical hits; SAH regroups
+ * them so fewer nodes are visited. */
+enum rt_bvh_layout {
+    RT_BVH_REFERENCE = 0, /* the BVH.py tree as exported */
+    RT_BVH_SAH = 1        /* surface-area-heuristic regrouping (default) */
+};
+
 /* Create a context on n_devices HIP devices (device_ids may be NULL = 0..n-1).
  * Replaces the pyopencl Context/CommandQueue/Program build of
  * KernelLauncher.__init__ (KernelLauncher.py:8-31). */
@@ -64,8 +72,8 @@ int rt_set_scene(rt_ctx* ctx, const float* vp, int64_t nvp, const float* vn, int
  * cl.Image of KernelLauncher.py:71-72). */
 int rt_set_env(rt_ctx* ctx, const uint8_t* rgba, int w, int h);
 
-/* Integer options: "traversal" (rt_traversal), "block" (threads per block:
- * 64, 128 or 256). */
+/* Integer options: "traversal" (rt_traversal), "bvh" (rt_bvh_layout; may be
+ * changed after rt_set_scene), "block" (threads per block: 64, 128 or 256). */
 int rt_set_option(rt_ctx* ctx, const char* key, int64_t value);
 
 /* Render one frame, blocking, into caller-owned host memory out_rgb[3*npix]
@@ -98,9 +106,10 @@ int64_t rt_tile_rows(int64_t npix, int width, int row0, int row_step);
 int rt_count_work(rt_ctx* ctx, const float cam[10], const float env[5], int64_t npix, int spp,
                   int max_bounce, int row0, int row_step, uint64_t counts[5]);
 
-/* Bytes the chosen traversal reads per unit of the counters above
- * (out[0..3] = per node fetch, per triangle test, per ray hit record, per
- * environment lookup). */
+/* Algorithmic bytes per unit of the counters above:
+ * out[0] = per node fetch (32 B per box tested: 64 for a FAST node, which
+ * tests both children; 32 for a REF node), out[1] = 36 per triangle test,
+ * out[2] = 40 per ray hit record, out[3] = 16 per environment lookup. */
 int rt_work_bytes(rt_ctx* ctx, double out[4]);
 
 /* Gamma kernel of ImgProcessing.cl:1-10: out[k] = powr(min(in[k],1), 2.2)

@@ -27,6 +27,14 @@ int rt_debug_trace(rt_ctx* ctx, int traversal, const float* rays, float* out, in
 int rt_debug_pixel_log(rt_ctx* ctx, int traversal, const float cam[10], const float env[5], int64_t npix, int spp,
                        int max_bounce, int64_t pixel, float* log, int cap, int* n_events, float out3[3]);
 
+/* rt_count_work's five counters for the whole frame plus two wave-level
+ * ones: out[5] = traversal-loop iterations issued by waves (an iteration
+ * counts once per wave however many lanes take part), out[6] = render-loop
+ * iterations of all waves.  out[0] + out[1] over 64 * out[5] is the SIMD
+ * efficiency of the traversal loop. */
+int rt_debug_wave_counts(rt_ctx* ctx, const float cam[10], const float env[5], int64_t npix, int spp,
+                         int max_bounce, uint64_t out[7]);
+
 /* Scene facts: out[0] = FAST layout available (1/0), out[1] = FAST stack
  * depth, out[2] = internal nodes, out[3] = triangles. */
 int rt_debug_scene_info(rt_ctx* ctx, int64_t out[4]);

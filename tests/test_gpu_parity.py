@@ -106,6 +106,60 @@ def test_trace_matches_reference_kat(kl, kat_ref, scene, traversal):
     np.testing.assert_array_equal(mats, ref[hit, 4])
 
 
+@pytest.mark.parametrize("scene", ["cornell", "monkey", "serre", "proto"])
+def test_trace_kat_with_reference_tree(kl, kat_ref, scene):
+    """FAST traversal over the exported BVH.py tree (not the SAH regrouping) vs the reference KAT."""
+    sc = W.load_scene(scene)
+    ctx = kl.native
+    ctx.set_scene(sc.V_p, sc.V_n, sc.V_uv, sc.faceData, sc.materialData, sc.BVH.exportArray)
+    kl._scene_key = None
+    try:
+        ctx.set_option("bvh", _native.RT_BVH_REFERENCE)
+        got = ctx.debug_trace(kat_ref[f"trace_{scene}_rays"], _native.RT_TRAVERSAL_FAST)
+    finally:
+        ctx.set_option("bvh", _native.RT_BVH_SAH)
+    ref = kat_ref[f"trace_{scene}_out"]
+    hit = got[:, 1] >= 0
+    np.testing.assert_array_equal(hit, ref[:, 5] == 1)
+    np.testing.assert_array_equal(got[hit, 0], ref[hit, 3])
+
+
+@pytest.mark.parametrize("case", ["cornell_128_s16", "monkey_c3_64_s4", "serre_96x54_s4", "furnace_64_s4"])
+def test_bvh_layouts_render_identically(kl, case):
+    """The SAH regrouping keeps every leaf box, so both trees give the same frame bit for bit."""
+    sc, cam, env, npix, spp, mb, ibl = W.PARITY_CASES[case].inputs()
+    a = _launch(kl, sc, cam, env, npix, spp, mb, ibl, "fast")
+    kl.set_bvh("reference")
+    try:
+        b = _launch(kl, sc, cam, env, npix, spp, mb, ibl, "fast")
+        ref_counts = kl.native.count_work(cam, env, npix, spp, mb)
+    finally:
+        kl.set_bvh("sah")
+    np.testing.assert_array_equal(a, b)
+    sah_counts = kl.native.count_work(cam, env, npix, spp, mb)
+    assert sah_counts["rays"] == ref_counts["rays"]
+    assert sah_counts["node_fetches"] <= ref_counts["node_fetches"]
+
+
+def test_wave_counters_are_consistent(kl):
+    sc, cam, env, npix, spp, mb, ibl = W.PARITY_CASES["cornell_64_s4"].inputs()
+    _launch(kl, sc, cam, env, npix, spp, mb, ibl, "fast")
+    wc = kl.native.wave_counts(cam, env, npix, spp, mb)
+    cw = kl.native.count_work(cam, env, npix, spp, mb)
+    for k in cw:
+        assert wc[k] == cw[k], k
+    lane_iters = wc["node_fetches"] + wc["tri_tests"]
+    assert wc["wave_trav_iters"] * 64 >= lane_iters > 0
+    assert wc["wave_render_iters"] * 64 >= wc["rays"]
+
+
+def test_bvh_option_errors(kl):
+    with pytest.raises(_native.NativeError, match="bvh"):
+        kl.native.set_option("bvh", 7)
+    with pytest.raises(ValueError):
+        kl.set_bvh("octree")
+
+
 @pytest.mark.parametrize("row_step", [2, 3, 8])
 def test_row_tiles_assemble_to_the_full_frame(kl, row_step):
     import torch

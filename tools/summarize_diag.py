@@ -2,7 +2,7 @@
 import csv, glob, sys, collections
 import numpy as np
 prof = sys.argv[1]
-kern = sys.argv[2] if len(sys.argv) > 2 else "render_kernel<0, false, false>"
+kern = sys.argv[2] if len(sys.argv) > 2 else "render_kernel<0, false, false"
 vals = collections.defaultdict(list)
 for p in glob.glob(prof + "/*/*counter_collection.csv"):
     for r in csv.DictReader(open(p, newline="")):

@@ -17,7 +17,7 @@ import sys
 import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-KERNEL = "render_kernel<0, false, false>"
+KERNEL = "render_kernel<0, false, false"  # FAST, uninstrumented (any SMEM variant)
 
 
 def _rows(pattern):

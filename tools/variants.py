@@ -30,7 +30,7 @@ from ensem3a_openclraytracer_amd import workloads as W
 from ensem3a_openclraytracer_amd.KernelLauncher import KernelLauncher
 import oracle.oracle as O
 from oracle import compare
-kl = KernelLauncher(traversal=os.environ.get("TRAV", "fast"))
+kl = KernelLauncher(traversal=os.environ.get("TRAV", "fast"), bvh=os.environ.get("BVH", "sah"))
 res = {}
 for case in ["furnace_64_s4", "monkey_c3_64_s4", "serre_96x54_s4", "proto_64_s4", "cornell_128_s16"]:
     sc, cam, env, npix, spp, mb, ibl = W.PARITY_CASES[case].inputs()
@@ -51,7 +51,7 @@ def run(names):
         r = subprocess.run([sys.executable, "-c", CHECK], env=env, capture_output=True, text=True, timeout=300)
         parity = r.stdout.strip().splitlines()[-1] if r.returncode == 0 else "ERR " + r.stderr[-300:]
         b = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "10", "--warmup", "2",
-                            "--no-cpu-baseline"], env=env, capture_output=True, text=True, timeout=300)
+                            "--no-cpu-baseline", "--bvh", os.environ.get("BVH", "sah")], env=env, capture_output=True, text=True, timeout=300)
         try:
             d = json.loads(b.stdout.strip().splitlines()[-1])
             perf = f'{d["value"]:.1f} Msamples/s kernel {d["roofline"]["kernel_ms"]:.3f} ms'
