@@ -23,6 +23,10 @@
 #include "bvh_sah.h"
 #include "rt_internal.h"
 
+#ifndef RT_BRUTE_MAX_DEFAULT
+#define RT_BRUTE_MAX_DEFAULT 64   // FAST tests every triangle of scenes up to this size (rt_set_option "brute_max")
+#endif
+
 namespace {
 
 thread_local std::string g_thread_error;
@@ -35,7 +39,7 @@ struct DevBuf {
 struct Device {
     int id = 0;
     hipStream_t stream = nullptr;
-    DevBuf nodes, bvh9, tri_geo, tri_shade, tri_frame, mat, ibl, out, counts, work, scratch_a, scratch_b;
+    DevBuf nodes, brute, bvh9, tri_geo, tri_shade, tri_frame, mat, ibl, out, counts, work, scratch_a, scratch_b;
     float* host_stage = nullptr;  // pinned staging for rt_render
     size_t host_stage_bytes = 0;
 };
@@ -47,6 +51,8 @@ struct HostScene {
     std::vector<float> tri_geo;    // 12 floats per triangle
     std::vector<float> tri_shade;  // 4 floats per triangle
     std::vector<float> mat;
+    std::vector<float> brute;      // 16 floats per triangle, small scenes only (rt_internal.h DevScene::brute)
+    int32_t nbrute = 0;
     int32_t nnodes = 0, root_ref = 0, ntri = 0, nmat = 0, nbvh9 = 0, depth = 1;
     float root_box[6] = {0, 0, 0, 0, 0, 0};
     bool fast_ok = false;
@@ -62,6 +68,7 @@ struct rt_ctx {
     int ibl_w = 0, ibl_h = 0;
     int traversal = RT_TRAVERSAL_FAST;
     int bvh_layout = RT_BVH_SAH;
+    int brute_max = RT_BRUTE_MAX_DEFAULT;
     int block = 128;
     std::string err;
 };
@@ -159,11 +166,11 @@ void emit_bvh2(HostScene& hs, const int32_t* L, const int32_t* R, const int32_t*
         o[0] = c0[0]; o[1] = c0[3]; o[2] = c0[1]; o[3] = c0[4];
         o[4] = c1[0]; o[5] = c1[3]; o[6] = c1[1]; o[7] = c1[4];
         o[8] = c0[2]; o[9] = c0[5]; o[10] = c1[2]; o[11] = c1[5];
-        const int32_t r0 = is_inner(L[n]) ? wide_of[L[n]] : ~T[L[n]];
-        const int32_t r1 = is_inner(R[n]) ? wide_of[R[n]] : ~T[R[n]];
+        const int32_t r0 = is_inner(L[n]) ? wide_of[L[n]] : ~(48 * T[L[n]]);
+        const int32_t r1 = is_inner(R[n]) ? wide_of[R[n]] : ~(48 * T[R[n]]);
         o[12] = as_f32(r0); o[13] = as_f32(r1); o[14] = 0.0f; o[15] = 0.0f;
     }
-    hs.root_ref = is_inner(0) ? 0 : ~T[0];
+    hs.root_ref = is_inner(0) ? 0 : ~(48 * T[0]);
     for (int k = 0; k < 6; ++k) hs.root_box[k] = box[k];
     hs.depth = max_depth;
 }
@@ -173,9 +180,14 @@ void emit_bvh2(HostScene& hs, const int32_t* L, const int32_t* R, const int32_t*
 // leaf, in which case only the REF traversal is available.  layout
 // RT_BVH_REFERENCE keeps the reference's tree, RT_BVH_SAH regroups its leaf
 // boxes (bvh_sah.cpp); both give the same hits.
-bool pack_fast(HostScene& hs, const float* bvh9, int64_t nn, int64_t ntri, int layout, std::string& why) {
+bool pack_fast(HostScene& hs, const float* bvh9, int64_t nn, int64_t ntri, int layout, int brute_max,
+               std::string& why) {
     if (nn <= 0) {
         why = "empty BVH";
+        return false;
+    }
+    if (ntri > 0x7fffffff / 48) {  // leaf refs are ~(48 * triangle)
+        why = "more than 44.7M triangles";
         return false;
     }
     std::vector<int32_t> L(nn), R(nn), T(nn);
@@ -236,6 +248,25 @@ bool pack_fast(HostScene& hs, const float* bvh9, int64_t nn, int64_t ntri, int l
         }
     }
     for (int64_t t = 0; t < ntri; ++t) hs.tri_geo[12 * t + 3] = as_f32(rank[t]);
+    // small scenes: brute-force records of the reachable triangles in DFS-rank order
+    hs.brute.clear();
+    hs.nbrute = 0;
+    if ((int64_t)leaves.size() <= (int64_t)brute_max) {
+        std::vector<int32_t> by_rank(leaves.size());
+        for (int32_t n : leaves) by_rank[rank[T[n]]] = n;
+        hs.brute.assign(16 * by_rank.size(), 0.0f);
+        for (size_t q = 0; q < by_rank.size(); ++q) {
+            const float* nd = bvh9 + 9 * (int64_t)by_rank[q];
+            const int32_t t = T[by_rank[q]];
+            const float* g = hs.tri_geo.data() + 12 * t;
+            float* r = hs.brute.data() + 16 * q;
+            r[0] = nd[2]; r[1] = nd[3]; r[2] = nd[4]; r[3] = nd[5];      // lo.xyz hi.x
+            r[4] = nd[6]; r[5] = nd[7]; r[6] = g[0]; r[7] = g[1];        // hi.yz a.xy
+            r[8] = g[2]; r[9] = g[4]; r[10] = g[5]; r[11] = g[6];        // a.z e1.xyz
+            r[12] = g[8]; r[13] = g[9]; r[14] = g[10]; r[15] = as_f32(t); // e2.xyz tri
+        }
+        hs.nbrute = (int32_t)by_rank.size();
+    }
     if (layout == RT_BVH_SAH && leaves.size() > 1) {
         std::vector<float> lb(6 * leaves.size());
         std::vector<int32_t> ids(leaves.size());
@@ -257,14 +288,17 @@ bool pack_fast(HostScene& hs, const float* bvh9, int64_t nn, int64_t ntri, int l
 }
 
 // pack_fast + the limits of the FAST kernels; sets hs.fast_ok.
-void pack_checked(HostScene& hs, const float* bvh9, int64_t nb, int64_t ntri, int layout, std::string& why) {
-    hs.fast_ok = (ntri > 0) ? pack_fast(hs, bvh9, nb, ntri, layout, why) : true;
-    if (ntri == 0) { hs.nnodes = 0; hs.root_ref = 0; hs.depth = 1; hs.nodes.clear(); }
+void pack_checked(HostScene& hs, const float* bvh9, int64_t nb, int64_t ntri, int layout, int brute_max,
+                  std::string& why) {
+    hs.fast_ok = (ntri > 0) ? pack_fast(hs, bvh9, nb, ntri, layout, brute_max, why) : true;
+    if (ntri == 0) { hs.nnodes = 0; hs.root_ref = 0; hs.depth = 1; hs.nodes.clear(); hs.brute.clear(); hs.nbrute = 0; }
+    if (!hs.fast_ok) { hs.brute.clear(); hs.nbrute = 0; }
     if (hs.fast_ok && (int64_t)hs.depth * 256 * 8 > 64 * 1024) {  // int2 stack entries, block <= 256
         hs.fast_ok = false;
         why = "tree too deep for the LDS stack";
     }
     if (hs.nodes.empty()) hs.nodes.assign(16, 0.0f);
+    if (hs.brute.empty()) hs.brute.assign(16, 0.0f);
 }
 
 template <typename T>
@@ -293,6 +327,8 @@ rt::DevScene dev_scene(const rt_ctx* ctx, const Device& d) {
     s.ibl_w = ctx->ibl_w;
     s.ibl_h = ctx->ibl_h;
     s.depth = ctx->hs.depth;
+    s.brute = (const float4*)d.brute.p;
+    s.nbrute = ctx->hs.nbrute;
     return s;
 }
 
@@ -370,7 +406,7 @@ void rt_destroy(rt_ctx* ctx) {
     for (auto& d : ctx->devs) {
         if (hipSetDevice(d.id) != hipSuccess) continue;
         if (d.stream) (void)hipStreamSynchronize(d.stream);
-        for (DevBuf* b : {&d.nodes, &d.bvh9, &d.tri_geo, &d.tri_shade, &d.tri_frame, &d.mat, &d.ibl, &d.out,
+        for (DevBuf* b : {&d.nodes, &d.brute, &d.bvh9, &d.tri_geo, &d.tri_shade, &d.tri_frame, &d.mat, &d.ibl, &d.out,
                           &d.counts, &d.work, &d.scratch_a, &d.scratch_b})
             release(*b);
         if (d.host_stage) (void)hipHostFree(d.host_stage);
@@ -389,17 +425,23 @@ int rt_set_option(rt_ctx* ctx, const char* key, int64_t value) {
         ctx->traversal = (int)value;
         return RT_OK;
     }
-    if (!std::strcmp(key, "bvh")) {
-        if (value != RT_BVH_REFERENCE && value != RT_BVH_SAH)
-            return set_err(ctx, RT_ERR_ARG, "bvh must be 0 (reference tree) or 1 (sah)");
-        ctx->bvh_layout = (int)value;
+    if (!std::strcmp(key, "bvh") || !std::strcmp(key, "brute_max")) {
+        if (!std::strcmp(key, "bvh")) {
+            if (value != RT_BVH_REFERENCE && value != RT_BVH_SAH)
+                return set_err(ctx, RT_ERR_ARG, "bvh must be 0 (reference tree) or 1 (sah)");
+            ctx->bvh_layout = (int)value;
+        } else {
+            if (value < 0 || value > 4096) return set_err(ctx, RT_ERR_ARG, "brute_max must be in 0..4096");
+            ctx->brute_max = (int)value;
+        }
         if (!ctx->have_scene) return RT_OK;
         HostScene& hs = ctx->hs;   // repack the FAST nodes of the current scene
         std::string why;
-        pack_checked(hs, hs.bvh9.data(), hs.nbvh9, hs.ntri, ctx->bvh_layout, why);
+        pack_checked(hs, hs.bvh9.data(), hs.nbvh9, hs.ntri, ctx->bvh_layout, ctx->brute_max, why);
         for (auto& d : ctx->devs) {
             HIP_OR_RET(ctx, hipSetDevice(d.id));
             HIP_OR_RET(ctx, upload(d.nodes, hs.nodes, d.stream));
+            HIP_OR_RET(ctx, upload(d.brute, hs.brute, d.stream));
             HIP_OR_RET(ctx, upload(d.tri_geo, hs.tri_geo, d.stream));
             HIP_OR_RET(ctx, hipStreamSynchronize(d.stream));
         }
@@ -493,10 +535,11 @@ int rt_set_scene(rt_ctx* ctx, const float* vp, int64_t nvp, const float* vn, int
         }
     }
     std::string why;
-    pack_checked(hs, bvh9, NB, T, ctx->bvh_layout, why);
+    pack_checked(hs, bvh9, NB, T, ctx->bvh_layout, ctx->brute_max, why);
     for (auto& d : ctx->devs) {
         HIP_OR_RET(ctx, hipSetDevice(d.id));
         HIP_OR_RET(ctx, upload(d.nodes, hs.nodes, d.stream));
+        HIP_OR_RET(ctx, upload(d.brute, hs.brute, d.stream));
         HIP_OR_RET(ctx, upload(d.bvh9, hs.bvh9, d.stream));
         HIP_OR_RET(ctx, upload(d.tri_geo, hs.tri_geo, d.stream));
         HIP_OR_RET(ctx, upload(d.tri_shade, hs.tri_shade, d.stream));

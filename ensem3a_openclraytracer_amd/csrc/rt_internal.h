@@ -12,10 +12,10 @@ struct DevScene {
     //   [0] = c0.min.x, c0.max.x, c0.min.y, c0.max.y
     //   [1] = c1.min.x, c1.max.x, c1.min.y, c1.max.y
     //   [2] = c0.min.z, c0.max.z, c1.min.z, c1.max.z
-    //   [3] = child refs (int bits): >= 0 internal node, < 0 leaf = ~triangle
+    //   [3] = child refs (int bits): >= 0 internal node, < 0 leaf = ~(48 * triangle), its tri_geo byte offset
     const float4* nodes;
     int32_t nnodes;        // internal nodes in `nodes`
-    int32_t root_ref;      // ref of the root (~tri when the root is a leaf)
+    int32_t root_ref;      // ref of the root (~(48 * tri) when the root is a leaf)
     float root_box[6];     // min.xyz, max.xyz of the root
     // REF traversal: the reference's own AoS export, 9 floats per node
     const float* bvh9;
@@ -34,6 +34,10 @@ struct DevScene {
     const uchar4* ibl;
     int32_t ibl_w, ibl_h;
     int32_t depth;         // max number of FAST stack entries a ray can need
+    // FAST on small scenes: one 64-byte record per reachable triangle in reference DFS order
+    // (leaf box, a.p, e1, e2, triangle index); nbrute = 0 when the BVH path is used
+    const float4* brute;
+    int32_t nbrute;
 };
 
 struct FrameParams {

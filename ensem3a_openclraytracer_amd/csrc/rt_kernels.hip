@@ -160,15 +160,19 @@ __device__ __forceinline__ void slab_fma(float lo_x, float hi_x, float lo_y, flo
 }
 
 constexpr float CULL_MARGIN = 1.0f + 0x1p-12f;
+#ifndef RT_HIT3
+#define RT_HIT3 1
+#endif
 
 // Branch-free Moller-Trumbore (same arithmetic as mt_test): all three loads are
 // issued together and one predicate decides, so a wave pays one memory round trip
 // and no nested divergence per triangle.
-__device__ __forceinline__ bool mt_flat(const float4* __restrict__ tg, int t, rtm_f3 o, rtm_f3 d, float* kout,
+// tb + toff: the triangle's 48-byte record (toff = 48 * t, 32-bit: no 64-bit multiply in the loop).
+__device__ __forceinline__ bool mt_flat(const char* __restrict__ tb, unsigned toff, rtm_f3 o, rtm_f3 d, float* kout,
                                         int* rank) {
-    const float4 g0 = tg[3 * t + 0];
-    const float4 g1 = tg[3 * t + 1];
-    const float4 g2 = tg[3 * t + 2];
+    const float4 g0 = *reinterpret_cast<const float4*>(tb + toff);
+    const float4 g1 = *reinterpret_cast<const float4*>(tb + toff + 16);
+    const float4 g2 = *reinterpret_cast<const float4*>(tb + toff + 32);
     const rtm_f3 e1 = xyz(g1), e2 = xyz(g2);
     const rtm_f3 h = rtm_cross(d, e2);
     const float a = rtm_dot(e1, h);
@@ -195,7 +199,16 @@ __device__ Hit trace_fast(const DevScene& S, const float4* __restrict__ nodes, c
     int best_rank = -1;
     if (COUNT) c.rays++;
     if (S.ntri <= 0) return best;
-    int2* __restrict__ stk = reinterpret_cast<int2*>(stk_base - threadIdx.x) + threadIdx.x;
+    // Stack entries int2 (ref, tmin bits) at [depth][B] in LDS, addressed by a running byte offset
+    // (push: += 8B, pop: -= 8B), node and triangle records by 32-bit byte offsets: the loop has no
+    // integer multiplies.
+    char* const sb = reinterpret_cast<char*>(stk_base - threadIdx.x) + 8 * threadIdx.x;
+    const unsigned sstride = 8u * (unsigned)B;
+    const char* const nb = reinterpret_cast<const char*>(nodes);
+    const char* const tb = reinterpret_cast<const char*>(tris);
+    // AoS: node i = 64 bytes at 64 i; SOA (LDS copy): plane k of node i at 16 (k nnodes + i), so
+    // 16 lanes reading 16 different nodes hit 16 different bank groups
+    const unsigned kstride = SOA ? 16u * (unsigned)S.nnodes : 16u;
     const float ix = 1.0f / d.x, iy = 1.0f / d.y, iz = 1.0f / d.z;
     const float oix = o.x * ix, oiy = o.y * iy, oiz = o.z * iz;
     float tmin, tmax;
@@ -203,60 +216,114 @@ __device__ Hit trace_fast(const DevScene& S, const float4* __restrict__ nodes, c
              ix, iy, iz, oix, oiy, oiz, tmin, tmax);
     if (!(tmax >= tmin && tmax >= 0.0f)) return best;
     int item = S.root_ref;
-    int sp = 0;
+    unsigned soff = 0;
     while (true) {
         if (COUNT) count_wave(c.wave_trav);
         if (item >= 0) {
             if (COUNT) c.nodes++;
-            // AoS: node i = nodes[4i .. 4i+3]; SOA (LDS copy): plane k at nodes[k * nnodes + i], so
-            // 16 lanes reading 16 different nodes hit 16 different bank groups
-            const float4* np = SOA ? nodes + item : nodes + 4 * item;
-            const int ks = SOA ? S.nnodes : 1;
-            const float4 a = np[0];
-            const float4 b = np[ks];
-            const float4 z = np[2 * ks];
-            const float4 e = np[3 * ks];
+            const char* np = nb + (SOA ? 16u : 64u) * (unsigned)item;
+            const float4 a = *reinterpret_cast<const float4*>(np);
+            const float4 b = *reinterpret_cast<const float4*>(np + kstride);
+            const float4 z = *reinterpret_cast<const float4*>(np + 2 * kstride);
+            const int2 e = *reinterpret_cast<const int2*>(np + 3 * kstride);
             float t0n, t0x, t1n, t1x;
             slab_fma(a.x, a.y, a.z, a.w, z.x, z.y, o.x, o.y, o.z, ix, iy, iz, oix, oiy, oiz, t0n, t0x);
             slab_fma(b.x, b.y, b.z, b.w, z.z, z.w, o.x, o.y, o.z, ix, iy, iz, oix, oiy, oiz, t1n, t1x);
             const float cull = best.k * CULL_MARGIN;
+#if RT_HIT3
+            // t0x >= t0n && t0x >= 0 && t0n <= cull, for the never-NaN slab values and cull > 0
+            const bool h0 = fmaxf(t0n, 0.0f) <= fminf(t0x, cull);
+            const bool h1 = fmaxf(t1n, 0.0f) <= fminf(t1x, cull);
+#else
             const bool h0 = t0x >= t0n && t0x >= 0.0f && t0n <= cull;
             const bool h1 = t1x >= t1n && t1x >= 0.0f && t1n <= cull;
-            const int r0 = __float_as_int(e.x), r1 = __float_as_int(e.y);
+#endif
             if (h0 && h1) {
                 const bool first0 = t0n <= t1n;
-                stk[sp * B] = make_int2(first0 ? r1 : r0, __float_as_int(first0 ? t1n : t0n));
-                ++sp;
-                item = first0 ? r0 : r1;
+                *reinterpret_cast<int2*>(sb + soff) = make_int2(first0 ? e.y : e.x, __float_as_int(first0 ? t1n : t0n));
+                soff += sstride;
+                item = first0 ? e.x : e.y;
                 continue;
             }
             if (h0 || h1) {
-                item = h0 ? r0 : r1;
+                item = h0 ? e.x : e.y;
                 continue;
             }
         } else {
             if (COUNT) c.tris++;
             float k;
             int rank;
-            const int t = ~item;
-            if (mt_flat(tris, t, o, d, &k, &rank) && k > 0.0001f &&
+            const unsigned toff = ~(unsigned)item;   // leaf ref = ~(48 * triangle)
+            if (mt_flat(tb, toff, o, d, &k, &rank) && k > 0.0001f &&
                 (k < best.k || (k == best.k && rank < best_rank))) {
                 best.k = k;
-                best.tri = t;
+                best.tri = (int)toff;
                 best_rank = rank;
             }
         }
         // pop the next item still in front of the best hit
         item = 0x7fffffff;
-        while (sp > 0) {
-            --sp;
-            const int2 en = stk[sp * B];
+        while (soff > 0) {
+            soff -= sstride;
+            const int2 en = *reinterpret_cast<const int2*>(sb + soff);
             if (__int_as_float(en.y) <= best.k * CULL_MARGIN) {
                 item = en.x;
                 break;
             }
         }
         if (item == 0x7fffffff) break;
+    }
+    if (best.tri >= 0) best.tri = (int)((unsigned)best.tri / 48u);
+    return best;
+}
+
+// Scenes of at most RT_BRUTE_MAX triangles: every lane of the wave tests the
+// same triangle at the same time, its record read once per wave through scalar
+// loads (SGPR operands, no LDS, no stack, no divergence).  The set of accepted
+// triangles is FAST's (own leaf box passes with the same slab arithmetic, MT
+// hit, k > 1e-4), and records are in the reference's DFS order, so the strict
+// `<` keeps the lowest rank on equal distances: the same hit as trace_fast.
+// Record (4 x float4): lo.xyz hi.x | hi.yz a.xy | a.z e1.xyz | e2.xyz tri.
+__device__ __forceinline__ float sgpr1(float x) {
+    return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(x)));
+}
+__device__ __forceinline__ float4 sgpr4(float4 v) {
+    return make_float4(sgpr1(v.x), sgpr1(v.y), sgpr1(v.z), sgpr1(v.w));
+}
+
+template <bool COUNT>
+__device__ Hit trace_brute(const DevScene& S, rtm_f3 o, rtm_f3 d, Cnt& c) {
+    Hit best{1000.0f, -1};
+    if (COUNT) c.rays++;
+    const float ix = 1.0f / d.x, iy = 1.0f / d.y, iz = 1.0f / d.z;
+    const float oix = o.x * ix, oiy = o.y * iy, oiz = o.z * iz;
+    for (int q = 0; q < S.nbrute; ++q) {
+        if (COUNT) count_wave(c.wave_trav);
+        // the record is wave-uniform: readfirstlane pins it in SGPRs (one s_load_dwordx16, SGPR
+        // operands).  Prefetching the next record costs more SALU moves than the latency it hides.
+        const float4 r0 = sgpr4(S.brute[4 * q + 0]), r1 = sgpr4(S.brute[4 * q + 1]);
+        const float4 r2 = sgpr4(S.brute[4 * q + 2]), r3 = sgpr4(S.brute[4 * q + 3]);
+        float tn, tx;
+        slab_fma(r0.x, r0.w, r0.y, r1.x, r0.z, r1.y, o.x, o.y, o.z, ix, iy, iz, oix, oiy, oiz, tn, tx);
+        const bool pass = fmaxf(tn, 0.0f) <= fminf(tx, best.k * CULL_MARGIN);
+        if (COUNT) c.nodes++;
+        if (__ballot(pass) == 0) continue;   // wave-uniform: nobody's box is hit
+        if (COUNT && pass) c.tris++;
+        const rtm_f3 a = rtm_v3(r1.z, r1.w, r2.x), e1 = rtm_v3(r2.y, r2.z, r2.w), e2 = rtm_v3(r3.x, r3.y, r3.z);
+        const rtm_f3 h = rtm_cross(d, e2);
+        const float det = rtm_dot(e1, h);
+        const float f = 1.0f / det;
+        const rtm_f3 sv = rtm_sub(o, a);
+        const float u = f * rtm_dot(sv, h);
+        const rtm_f3 qv = rtm_cross(sv, e1);
+        const float v = f * rtm_dot(d, qv);
+        const float k = f * rtm_dot(e2, qv);
+        const bool parallel = det > -0.0000001f && det < 0.0000001f;
+        const bool hit = !parallel && !(u < 0.0f || u > 1.0f) && !(v < 0.0f || u + v > 1.0f) && (k > 0.0000001f);
+        if (pass && hit && k > 0.0001f && k < best.k) {
+            best.k = k;
+            best.tri = __float_as_int(r3.w);
+        }
     }
     return best;
 }
@@ -265,6 +332,7 @@ template <int TRAV, bool COUNT, bool SOA = false>
 __device__ __forceinline__ Hit trace(const DevScene& S, const float4* nodes, const float4* tris, rtm_f3 o, rtm_f3 d,
                                      int* stk, int B, Cnt& c) {
     if (TRAV == TRAV_REF) return trace_ref<COUNT>(S, o, d, stk, B, c);
+    if (S.nbrute > 0) return trace_brute<COUNT>(S, o, d, c);
     return trace_fast<COUNT, SOA>(S, nodes, tris, o, d, stk, B, c);
 }
 
@@ -717,7 +785,8 @@ __global__ void gamma_kernel(const float* __restrict__ in, float* __restrict__ o
 template <int TRAV, bool COUNT, bool LOG, bool SMEM = false>
 hipError_t launch_t(const DevScene& sc, const FrameParams& fp, int block, float* d_out, unsigned long long* d_counts,
                     unsigned int* d_work, hipStream_t stream) {
-    const int depth = (TRAV == TRAV_REF) ? REF_STACK : 2 * (sc.depth > 0 ? sc.depth : 1);  // FAST: int2 entries
+    // FAST: int2 entries; the brute-force path of small scenes needs no stack
+    const int depth = (TRAV == TRAV_REF) ? REF_STACK : (sc.nbrute > 0 ? 1 : 2 * (sc.depth > 0 ? sc.depth : 1));
     size_t lds = (size_t)depth * block * sizeof(int);
     if (SMEM) lds += (size_t)(4 * sc.nnodes + 3 * sc.ntri) * sizeof(float4);
     const int64_t need = (fp.nloc + block - 1) / block;
@@ -820,7 +889,7 @@ hipError_t launch_render(const DevScene& sc, const FrameParams& fp, int traversa
                         : launch_t<TRAV_REF, false, false>(sc, fp, block, d_out, d_counts, d_work, stream);
     }
     const size_t scene_bytes = (size_t)(4 * sc.nnodes + 3 * sc.ntri) * sizeof(float4);
-    if (sc.ntri > 0 && scene_bytes <= (size_t)RT_LDS_SCENE_MAX) {
+    if (sc.ntri > 0 && sc.nbrute == 0 && scene_bytes <= (size_t)RT_LDS_SCENE_MAX) {
         return d_counts ? launch_t<TRAV_FAST, true, false, true>(sc, fp, block, d_out, d_counts, d_work, stream)
                         : launch_t<TRAV_FAST, false, false, true>(sc, fp, block, d_out, d_counts, d_work, stream);
     }

@@ -72,8 +72,11 @@ int rt_set_scene(rt_ctx* ctx, const float* vp, int64_t nvp, const float* vn, int
  * cl.Image of KernelLauncher.py:71-72). */
 int rt_set_env(rt_ctx* ctx, const uint8_t* rgba, int w, int h);
 
-/* Integer options: "traversal" (rt_traversal), "bvh" (rt_bvh_layout; may be
- * changed after rt_set_scene), "block" (threads per block: 64, 128 or 256). */
+/* Integer options: "traversal" (rt_traversal), "bvh" (rt_bvh_layout),
+ * "brute_max" (FAST on scenes of at most this many triangles tests every
+ * triangle in lock-step instead of walking the tree -- same hits; default 64,
+ * 0 = always walk the tree), "block" (threads per block: 64, 128 or 256).
+ * "bvh" and "brute_max" may be changed after rt_set_scene. */
 int rt_set_option(rt_ctx* ctx, const char* key, int64_t value);
 
 /* Render one frame, blocking, into caller-owned host memory out_rgb[3*npix]

@@ -141,6 +141,42 @@ def test_bvh_layouts_render_identically(kl, case):
     assert sah_counts["node_fetches"] <= ref_counts["node_fetches"]
 
 
+@pytest.mark.parametrize("case", ["cornell_64_s4", "cornell_128_s16", "cornell_64_b0"])
+def test_brute_force_path_matches_tree_walk(kl, case):
+    """Small scenes test every triangle in lock-step (brute_max); same frame as walking the SAH tree."""
+    sc, cam, env, npix, spp, mb, ibl = W.PARITY_CASES[case].inputs()
+    assert sc.faceData.size // 10 <= 64
+    a = _launch(kl, sc, cam, env, npix, spp, mb, ibl, "fast")
+    kl.native.set_option("brute_max", 0)
+    try:
+        b = _launch(kl, sc, cam, env, npix, spp, mb, ibl, "fast")
+        tree_counts = kl.native.count_work(cam, env, npix, spp, mb)
+    finally:
+        kl.native.set_option("brute_max", 64)
+    np.testing.assert_array_equal(a, b)
+    brute_counts = kl.native.count_work(cam, env, npix, spp, mb)
+    assert brute_counts["rays"] == tree_counts["rays"]
+    # brute force visits one box per triangle per ray
+    assert brute_counts["node_fetches"] == brute_counts["rays"] * (sc.faceData.size // 10)
+
+
+def test_brute_force_trace_kat(kl, kat_ref):
+    sc = W.load_scene("cornell")
+    ctx = kl.native
+    ctx.set_scene(sc.V_p, sc.V_n, sc.V_uv, sc.faceData, sc.materialData, sc.BVH.exportArray)
+    kl._scene_key = None
+    rays, ref = kat_ref["trace_cornell_rays"], kat_ref["trace_cornell_out"]
+    for bm in (64, 0):
+        ctx.set_option("brute_max", bm)
+        got = ctx.debug_trace(rays, _native.RT_TRAVERSAL_FAST)
+        hit = got[:, 1] >= 0
+        np.testing.assert_array_equal(hit, ref[:, 5] == 1)
+        np.testing.assert_array_equal(got[hit, 0], ref[hit, 3])
+    ctx.set_option("brute_max", 64)
+    with pytest.raises(_native.NativeError, match="brute_max"):
+        ctx.set_option("brute_max", -1)
+
+
 def test_wave_counters_are_consistent(kl):
     sc, cam, env, npix, spp, mb, ibl = W.PARITY_CASES["cornell_64_s4"].inputs()
     _launch(kl, sc, cam, env, npix, spp, mb, ibl, "fast")
