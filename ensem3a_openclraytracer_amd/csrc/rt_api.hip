@@ -23,6 +23,9 @@
 #include "bvh_sah.h"
 #include "rt_internal.h"
 
+#ifndef RT_RESUME_MIN_DEFAULT
+#define RT_RESUME_MIN_DEFAULT 40  // FAST tree walk: resumable traversal threshold (rt_set_option "resume_min")
+#endif
 #ifndef RT_BRUTE_MAX_DEFAULT
 #define RT_BRUTE_MAX_DEFAULT 64   // FAST tests every triangle of scenes up to this size (rt_set_option "brute_max")
 #endif
@@ -69,6 +72,7 @@ struct rt_ctx {
     int traversal = RT_TRAVERSAL_FAST;
     int bvh_layout = RT_BVH_SAH;
     int brute_max = RT_BRUTE_MAX_DEFAULT;
+    int resume_min = RT_RESUME_MIN_DEFAULT;
     int block = 128;
     std::string err;
 };
@@ -352,6 +356,7 @@ int check_frame(rt_ctx* ctx, const float* cam, const float* env, int64_t npix, i
     fp->row_step = row_step;
     fp->nloc = rt_tile_rows(npix, fp->width, row0, row_step) * fp->width;
     fp->log_pixel = -1;
+    fp->resume_min = ctx->resume_min;
     fp->log_buf = nullptr;
     fp->log_cap = 0;
     fp->log_count = nullptr;
@@ -446,6 +451,11 @@ int rt_set_option(rt_ctx* ctx, const char* key, int64_t value) {
             HIP_OR_RET(ctx, hipStreamSynchronize(d.stream));
         }
         if (!hs.fast_ok) ctx->err = "FAST traversal unavailable (" + why + "); REF traversal will be used";
+        return RT_OK;
+    }
+    if (!std::strcmp(key, "resume_min")) {
+        if (value < 0 || value > 64) return set_err(ctx, RT_ERR_ARG, "resume_min must be in 0..64");
+        ctx->resume_min = (int)value;
         return RT_OK;
     }
     if (!std::strcmp(key, "block")) {

@@ -25,6 +25,7 @@
 // Numerics: every OpenCL builtin of the reference is taken from rtm.h and the
 // file is compiled with -ffp-contract=off (see rtm.h).
 #include <algorithm>
+#include <climits>
 
 #include "rt_internal.h"
 #include "rtm.h"
@@ -774,6 +775,325 @@ __global__ void RT_RENDER_BOUNDS render_kernel(DevScene S, FrameParams F, float*
     }
 }
 
+// ---- resumable FAST traversal (option "resume_min") ----
+// On deep scenes a wave's traversal loop runs until its slowest ray is done
+// (SIMD efficiency 13 % on C3/C4).  Here each lane keeps its traversal state in
+// registers across render-loop iterations: the wave runs traversal rounds only
+// until at least F.resume_min lanes have no ray in flight, then those lanes shade
+// and start their next ray while the others continue where they stopped.
+struct FastRay {
+    rtm_f3 o, d;
+    float ix, iy, iz;
+    int item;
+    unsigned soff;    // stack top, bytes
+    float bk;         // best distance
+    int bt;           // best triangle's byte offset (48 t), -1 = none
+    int brank;        // its rank in the reference DFS order
+};
+
+// Returns true when the ray is already finished (no triangles / root box missed).
+template <bool COUNT>
+__device__ __forceinline__ bool fast_init(const DevScene& S, FastRay& R, rtm_f3 o, rtm_f3 d, Cnt& c) {
+    if (COUNT) c.rays++;
+    R.o = o;
+    R.d = d;
+    R.bk = 1000.0f;
+    R.bt = -1;
+    R.brank = -1;
+    R.soff = 0;
+    if (S.ntri <= 0) return true;
+    R.ix = 1.0f / d.x;
+    R.iy = 1.0f / d.y;
+    R.iz = 1.0f / d.z;
+    float tmin, tmax;
+    slab_fma(S.root_box[0], S.root_box[3], S.root_box[1], S.root_box[4], S.root_box[2], S.root_box[5], o.x, o.y, o.z,
+             R.ix, R.iy, R.iz, o.x * R.ix, o.y * R.iy, o.z * R.iz, tmin, tmax);
+    if (!(tmax >= tmin && tmax >= 0.0f)) return true;
+    R.item = S.root_ref;
+    return false;
+}
+
+// One round of trace_fast's loop: descend nearest children until a leaf is
+// tested or nothing is hit, then pop the next live stack entry.  Same
+// arithmetic and order as trace_fast.  Returns true when the ray is finished.
+template <bool COUNT, bool SOA>
+__device__ __forceinline__ bool fast_round(const DevScene& S, FastRay& R, const char* nb, const char* tb, char* sb,
+                                           unsigned sstride, unsigned kstride, Cnt& c) {
+    const float oix = R.o.x * R.ix, oiy = R.o.y * R.iy, oiz = R.o.z * R.iz;
+    while (R.item >= 0) {
+        if (COUNT) { count_wave(c.wave_trav); c.nodes++; }
+        const char* np = nb + (SOA ? 16u : 64u) * (unsigned)R.item;
+        const float4 a = *reinterpret_cast<const float4*>(np);
+        const float4 b = *reinterpret_cast<const float4*>(np + kstride);
+        const float4 z = *reinterpret_cast<const float4*>(np + 2 * kstride);
+        const int2 e = *reinterpret_cast<const int2*>(np + 3 * kstride);
+        float t0n, t0x, t1n, t1x;
+        slab_fma(a.x, a.y, a.z, a.w, z.x, z.y, R.o.x, R.o.y, R.o.z, R.ix, R.iy, R.iz, oix, oiy, oiz, t0n, t0x);
+        slab_fma(b.x, b.y, b.z, b.w, z.z, z.w, R.o.x, R.o.y, R.o.z, R.ix, R.iy, R.iz, oix, oiy, oiz, t1n, t1x);
+        const float cull = R.bk * CULL_MARGIN;
+        const bool h0 = fmaxf(t0n, 0.0f) <= fminf(t0x, cull);
+        const bool h1 = fmaxf(t1n, 0.0f) <= fminf(t1x, cull);
+        if (h0 && h1) {
+            const bool first0 = t0n <= t1n;
+            *reinterpret_cast<int2*>(sb + R.soff) = make_int2(first0 ? e.y : e.x, __float_as_int(first0 ? t1n : t0n));
+            R.soff += sstride;
+            R.item = first0 ? e.x : e.y;
+        } else if (h0 || h1) {
+            R.item = h0 ? e.x : e.y;
+        } else {
+            R.item = INT_MIN;      // nothing hit below this node: pop (never a leaf ref: those are ~(48 t))
+        }
+    }
+    if (R.item != INT_MIN) {      // a leaf: one triangle test
+        if (COUNT) { count_wave(c.wave_trav); c.tris++; }
+        float k;
+        int rank;
+        const unsigned toff = ~(unsigned)R.item;
+        if (mt_flat(tb, toff, R.o, R.d, &k, &rank) && k > 0.0001f &&
+            (k < R.bk || (k == R.bk && rank < R.brank))) {
+            R.bk = k;
+            R.bt = (int)toff;
+            R.brank = rank;
+        }
+    }
+    while (R.soff > 0) {   // pop the next item still in front of the best hit
+        R.soff -= sstride;
+        const int2 en = *reinterpret_cast<const int2*>(sb + R.soff);
+        if (__int_as_float(en.y) <= R.bk * CULL_MARGIN) {
+            R.item = en.x;
+            return false;
+        }
+    }
+    return true;
+}
+
+template <bool COUNT, bool LOG, bool SMEM>
+__global__ void RT_RENDER_BOUNDS render_resume_kernel(DevScene S, FrameParams F, float* __restrict__ out,
+                                                      unsigned long long* __restrict__ counts,
+                                                      unsigned int* __restrict__ work_counter,
+                                                      const LaunchConst* __restrict__ lconst) {
+    extern __shared__ int lds_stack[];
+    const int B = blockDim.x;
+    Cnt c{0, 0, 0, 0, 0, 0, 0};
+    const LaunchConst& C = *lconst;
+    const float4* nodes = S.nodes;
+    const float4* tris = S.tri_geo;
+    if (SMEM) {
+        float4* ln = reinterpret_cast<float4*>(lds_stack + 2 * S.depth * B);
+        float4* lt = ln + 4 * S.nnodes;
+        for (int q = threadIdx.x; q < 4 * S.nnodes; q += B) ln[(q & 3) * S.nnodes + (q >> 2)] = S.nodes[q];
+        for (int q = threadIdx.x; q < 3 * S.ntri; q += B) lt[q] = S.tri_geo[q];
+        __syncthreads();
+        nodes = ln;
+        tris = lt;
+    }
+    char* const sb = reinterpret_cast<char*>(lds_stack) + 8 * threadIdx.x;
+    const unsigned sstride = 8u * (unsigned)B;
+    const char* const nb = reinterpret_cast<const char*>(nodes);
+    const char* const tb = reinterpret_cast<const char*>(tris);
+    const unsigned kstride = SMEM ? 16u * (unsigned)S.nnodes : 16u;
+    const int W = F.width;
+    const int imgSize = (int)F.npix;
+    const float e3 = F.env[3], e4 = F.env[4];
+    const int spp = F.spp, maxB = F.max_bounce;
+    const unsigned int nloc = (unsigned int)F.nloc;
+    const int lane = threadIdx.x & 63;
+
+    int phase = FETCH;
+    bool tracing = false;
+    FastRay T;
+    T.item = 0; T.soff = 0; T.bk = 1000.0f; T.bt = -1; T.brank = -1;
+    T.o = rtm_v3(0, 0, 0); T.d = rtm_v3(0, 0, 1); T.ix = T.iy = T.iz = 0.0f;
+    int p = 0, i = 0;
+    bool logme = false;
+    uint32_t seed0 = 0, seed1 = 0;
+    rtm_f3 cd = rtm_v3(0, 0, 0);              // camera ray direction (origin = C.position)
+    float kc = 1000.0f;                       // cached primary hit (Raytracing.cl:186-187)
+    int tc = -1;
+    rtm_f3 Ro = rtm_v3(0, 0, 0), Rd = rtm_v3(0, 0, 0), so = rtm_v3(1, 1, 1);
+    float k = 1000.0f;
+    int tri = -1, j = 0;
+    rtm_f3 Bo = rtm_v3(0, 0, 0), Bd = rtm_v3(0, 0, 0);
+    rtm_f3 acc = rtm_v3(0, 0, 0);
+    int s = 0;
+
+    auto write_pixel = [&]() {
+        const rtm_f3 o = rtm_div(acc, (float)spp);   // mean + clamp, Raytracing.cl:211-220
+        float* dst = out + 3 * (int64_t)p;
+        dst[0] = rtm_fmax(rtm_fmin(o.x, 1.0f), 0.0f);
+        dst[1] = rtm_fmax(rtm_fmin(o.y, 1.0f), 0.0f);
+        dst[2] = rtm_fmax(rtm_fmin(o.z, 1.0f), 0.0f);
+    };
+    auto finish_sample = [&]() {  // output += baseColor; next sample from the cached camera hit
+        if (LOG && logme) log_event(F, 3.0f, s + 1, rtm_v3(0, 0, 0), rtm_v3(0, 0, 0), 0.0f, 0, so);
+        acc = rtm_add(acc, so);
+        ++s;
+        if (s >= spp) {
+            write_pixel();
+            phase = FETCH;
+        } else {
+            Ro = C.position; Rd = cd; tri = tc; k = kc; j = 0;
+            so = rtm_v3(1, 1, 1);
+            phase = PREP;
+        }
+    };
+    auto start = [&](rtm_f3 o, rtm_f3 d) {
+        tracing = !fast_init<COUNT>(S, T, o, d, c);
+    };
+
+    while (true) {
+        // -- refill: ballot the lanes that need a pixel, one atomic per wave --
+        const unsigned long long need = __ballot(phase == FETCH);
+        if (need) {
+            unsigned int base = 0;
+            const int leader = __ffsll((long long)need) - 1;
+            if (lane == leader) base = atomicAdd(work_counter, (unsigned int)__popcll(need));
+            base = __shfl(base, leader, 64);
+            if (phase == FETCH) {
+                const unsigned long long below = need & ((1ull << lane) - 1ull);
+                const unsigned int q = base + (unsigned int)__popcll(below);
+                bool ok = q < nloc;
+                if (ok) {
+                    p = (int)q;
+                    const int krow = p / W;
+                    const int col = p - krow * W;
+                    const int64_t i64 = ((int64_t)F.row0 + (int64_t)krow * F.row_step) * W + col;
+                    ok = i64 < F.npix;
+                    i = (int)i64;
+                }
+                if (ok) {
+                    seed0 = (uint32_t)(i % imgSize);
+                    seed1 = (uint32_t)(i / imgSize);
+                    cd = camera_dir(C, W, i);
+                    acc = rtm_v3(0, 0, 0);
+                    s = 0;
+                    phase = PRIMARY;
+                    logme = LOG && i == F.log_pixel;
+                    start(C.position, cd);
+                } else {
+                    phase = DONE;
+                }
+            }
+        }
+        if (__all(phase == DONE)) break;
+        if (COUNT && lane == 0) c.wave_outer++;
+
+        // -- advance every lane without a ray in flight until it needs one --
+        if (!tracing && phase != DONE && phase != FETCH) {
+            const Hit h{T.bk, T.bt >= 0 ? (int)((unsigned)T.bt / 48u) : -1};
+            if (phase == PRIMARY) {
+                tc = h.tri;
+                kc = h.k;
+                Ro = C.position; Rd = cd; tri = tc; k = kc; j = 0;
+                so = rtm_v3(1, 1, 1);
+                phase = PREP;
+                if (spp <= 0) {   // reference: output = 0/0 -> NaN -> clamp gives 1
+                    write_pixel();
+                    phase = FETCH;
+                }
+            } else if (phase == BOUNCE) {
+                if (LOG && logme) {
+                    const int hm = h.tri >= 0 ? __float_as_int(S.tri_shade[h.tri].w) : 0;
+                    log_event(F, 1.0f, j, Bo, Bd, h.tri >= 0 ? h.k : -1.0f, hm, so);
+                }
+                if (h.tri >= 0) {
+                    Ro = Bo; Rd = Bd; tri = h.tri; k = h.k;
+                    const Mat bm = load_mat(S.mat, __float_as_int(S.tri_shade[h.tri].w));
+                    if (bm.type != 0) {
+                        if (j == maxB) {
+                            so = rtm_v3(0, 0, 0);
+                            finish_sample();
+                        } else {
+                            ++j;
+                            phase = PREP;
+                        }
+                    } else {
+                        so = rtm_scale(so, bm.rough);
+                        finish_sample();
+                    }
+                } else {
+                    phase = SUN;   // escaped: shadow ray towards the sun (Raytracing.cl:115-124)
+                    start(Bo, C.sun);
+                    if (!tracing) continue;  // unreachable in practice (root box always hit from inside)
+                }
+            } else if (phase == SUN) {  // Raytracing.cl:125-137
+                if (LOG && logme) {
+                    const int hm = h.tri >= 0 ? __float_as_int(S.tri_shade[h.tri].w) : 0;
+                    log_event(F, 2.0f, j, Bo, C.sun, h.tri >= 0 ? h.k : -1.0f, hm, so);
+                }
+                rtm_f3 sunLight = rtm_v3(0, 0, 0);
+                const Mat cm = load_mat(S.mat, __float_as_int(S.tri_shade[tri].w));
+                if (h.tri < 0 && cm.type != 3) sunLight = rtm_v3(e3, e3, e3);
+                if (h.tri >= 0) {
+                    const Mat sm = load_mat(S.mat, __float_as_int(S.tri_shade[h.tri].w));
+                    if (sm.type == 3) sunLight = rtm_scale(sm.color, e3);
+                }
+                const rtm_f3 envLight = rtm_scale(sample_ibl<COUNT>(S, C, Bd, c), e4);
+                so = rtm_mul(so, rtm_add(sunLight, envLight));
+                finish_sample();
+            }
+            // naiveGI loop heads (Raytracing.cl:46-79) until a ray is needed or the pixel is done
+            while (phase == PREP) {
+                if (j > maxB) {
+                    finish_sample();   // naiveGI's loop never entered (maxBounce < 0): the sample stays 1
+                } else if (tri < 0) {
+                    so = rtm_scale(rtm_mul(so, sample_ibl<COUNT>(S, C, Rd, c)), e4);
+                    finish_sample();
+                } else {
+                    const float4 sh = S.tri_shade[tri];
+                    const rtm_f3 n = xyz(sh);
+                    const Mat cm = load_mat(S.mat, __float_as_int(sh.w));
+                    if (cm.type == 0) {
+                        so = rtm_scale(so, cm.rough);
+                        finish_sample();
+                    } else {
+                        const float4 f2 = S.tri_frame[3 * tri + 2];
+                        const rtm_f3 nn = xyz(f2);
+                        float invPdf = 0.0f;
+                        rtm_f3 brdf = rtm_v3(0, 0, 0);
+                        if (cm.type == 1) {
+                            Bd = hemi_cosine(n, S.tri_frame[3 * tri], S.tri_frame[3 * tri + 1], f2, &seed1, &seed0,
+                                             &invPdf);
+                            brdf = rtm_scale(cm.color, 1.0f / 3.14f);
+                        } else if (cm.type == 2) {
+                            Bd = hemi_uniform(n, S.tri_frame[3 * tri], S.tri_frame[3 * tri + 1], f2, &seed1, &seed0,
+                                              &invPdf);
+                            brdf = brdf_ggx(cm.color, cm.rough, rtm_scale(Rd, -1.0f), Bd, n);
+                        } else {
+                            Bd = Rd;
+                            brdf = cm.color;
+                            invPdf = 1.0f / rtm_fabs(rtm_dot(Bd, nn));
+                        }
+                        const rtm_f3 nd = rtm_normalize(Rd);
+                        Bo = rtm_v3(fmaf(nd.x, k, Ro.x), fmaf(nd.y, k, Ro.y), fmaf(nd.z, k, Ro.z));
+                        // attenuation depends only on pre-trace values (Raytracing.cl:86-87): apply now
+                        const float att = invPdf * rtm_fabs(rtm_dot(Bd, nn));
+                        so = rtm_scale(rtm_mul(so, brdf), att);
+                        phase = BOUNCE;
+                        start(Bo, Bd);
+                    }
+                }
+            }
+        }
+
+        // -- traversal rounds until at least F.resume_min lanes have no ray in flight --
+        while (true) {
+            if (tracing && fast_round<COUNT, SMEM>(S, T, nb, tb, sb, sstride, kstride, c)) tracing = false;
+            const unsigned long long tr = __ballot(tracing);
+            if (tr == 0 || 64 - __popcll(tr) >= F.resume_min) break;
+        }
+    }
+    if (COUNT) {
+        unsigned long long v[NCOUNTS] = {c.nodes, c.tris, c.rays, c.env, c.dropped, c.wave_trav, c.wave_outer};
+#pragma unroll
+        for (int q = 0; q < NCOUNTS; ++q) {
+            unsigned long long x = v[q];
+            for (int off = 32; off > 0; off >>= 1) x += __shfl_down(x, off, 64);
+            if (lane == 0 && x) atomicAdd(&counts[q], x);
+        }
+    }
+}
+
 __global__ void gamma_kernel(const float* __restrict__ in, float* __restrict__ out, int64_t n) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i < n) {
@@ -782,7 +1102,7 @@ __global__ void gamma_kernel(const float* __restrict__ in, float* __restrict__ o
     }
 }
 
-template <int TRAV, bool COUNT, bool LOG, bool SMEM = false>
+template <int TRAV, bool COUNT, bool LOG, bool SMEM = false, bool RESUME = false>
 hipError_t launch_t(const DevScene& sc, const FrameParams& fp, int block, float* d_out, unsigned long long* d_counts,
                     unsigned int* d_work, hipStream_t stream) {
     // FAST: int2 entries; the brute-force path of small scenes needs no stack
@@ -795,9 +1115,9 @@ hipError_t launch_t(const DevScene& sc, const FrameParams& fp, int block, float*
     int dev = 0, cus = 0, per_cu = 0;
     hipError_t e = hipGetDevice(&dev);
     if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    if (e == hipSuccess)
-        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)render_kernel<TRAV, COUNT, LOG, SMEM>,
-                                                         block, lds);
+    const void* kfn = RESUME ? (const void*)render_resume_kernel<COUNT, LOG, SMEM>
+                             : (const void*)render_kernel<TRAV, COUNT, LOG, SMEM>;
+    if (e == hipSuccess) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kfn, block, lds);
     if (e != hipSuccess) return e;
     const int64_t resident = (int64_t)std::max(1, cus) * std::max(1, per_cu);
     const int64_t grid = std::min(need, resident);
@@ -806,8 +1126,12 @@ hipError_t launch_t(const DevScene& sc, const FrameParams& fp, int block, float*
     // the per-launch constants live after the counter in the same scratch block
     LaunchConst* lc = reinterpret_cast<LaunchConst*>(reinterpret_cast<char*>(d_work) + 64);
     hipLaunchKernelGGL(make_const_kernel, dim3(1), dim3(64), 0, stream, fp, lc);
-    hipLaunchKernelGGL((render_kernel<TRAV, COUNT, LOG, SMEM>), dim3((unsigned)grid), dim3(block), lds, stream, sc,
-                       fp, d_out, d_counts, d_work, (const LaunchConst*)lc);
+    if (RESUME)
+        hipLaunchKernelGGL((render_resume_kernel<COUNT, LOG, SMEM>), dim3((unsigned)grid), dim3(block), lds, stream,
+                           sc, fp, d_out, d_counts, d_work, (const LaunchConst*)lc);
+    else
+        hipLaunchKernelGGL((render_kernel<TRAV, COUNT, LOG, SMEM>), dim3((unsigned)grid), dim3(block), lds, stream,
+                           sc, fp, d_out, d_counts, d_work, (const LaunchConst*)lc);
     return hipGetLastError();
 }
 
@@ -889,6 +1213,14 @@ hipError_t launch_render(const DevScene& sc, const FrameParams& fp, int traversa
                         : launch_t<TRAV_REF, false, false>(sc, fp, block, d_out, d_counts, d_work, stream);
     }
     const size_t scene_bytes = (size_t)(4 * sc.nnodes + 3 * sc.ntri) * sizeof(float4);
+    if (sc.ntri > 0 && sc.nbrute == 0 && fp.resume_min > 0) {
+        if (scene_bytes <= (size_t)RT_LDS_SCENE_MAX)
+            return d_counts ? launch_t<TRAV_FAST, true, false, true, true>(sc, fp, block, d_out, d_counts, d_work, stream)
+                            : launch_t<TRAV_FAST, false, false, true, true>(sc, fp, block, d_out, d_counts, d_work,
+                                                                            stream);
+        return d_counts ? launch_t<TRAV_FAST, true, false, false, true>(sc, fp, block, d_out, d_counts, d_work, stream)
+                        : launch_t<TRAV_FAST, false, false, false, true>(sc, fp, block, d_out, d_counts, d_work, stream);
+    }
     if (sc.ntri > 0 && sc.nbrute == 0 && scene_bytes <= (size_t)RT_LDS_SCENE_MAX) {
         return d_counts ? launch_t<TRAV_FAST, true, false, true>(sc, fp, block, d_out, d_counts, d_work, stream)
                         : launch_t<TRAV_FAST, false, false, true>(sc, fp, block, d_out, d_counts, d_work, stream);

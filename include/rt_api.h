@@ -75,7 +75,11 @@ int rt_set_env(rt_ctx* ctx, const uint8_t* rgba, int w, int h);
 /* Integer options: "traversal" (rt_traversal), "bvh" (rt_bvh_layout),
  * "brute_max" (FAST on scenes of at most this many triangles tests every
  * triangle in lock-step instead of walking the tree -- same hits; default 64,
- * 0 = always walk the tree), "block" (threads per block: 64, 128 or 256).
+ * 0 = always walk the tree),
+ * "resume_min" (FAST tree walk: 0 = each wave traces until all its rays are
+ * done; 1..64 = rays keep their traversal state across render-loop
+ * iterations and the wave shades as soon as this many lanes are free -- same
+ * hits), "block" (threads per block: 64, 128 or 256).
  * "bvh" and "brute_max" may be changed after rt_set_scene. */
 int rt_set_option(rt_ctx* ctx, const char* key, int64_t value);
 

@@ -177,6 +177,21 @@ def test_brute_force_trace_kat(kl, kat_ref):
         ctx.set_option("brute_max", -1)
 
 
+@pytest.mark.parametrize("case", ["monkey_c3_64_s4", "serre_96x54_s4", "proto_64_s4"])
+def test_resumable_traversal_matches_plain_walk(kl, case):
+    """resume_min (rays keep their traversal state across render-loop iterations) changes no hit."""
+    sc, cam, env, npix, spp, mb, ibl = W.PARITY_CASES[case].inputs()
+    frames = []
+    for t in (0, 1, 40, 64):
+        kl.native.set_option("resume_min", t)
+        frames.append(_launch(kl, sc, cam, env, npix, spp, mb, ibl, "fast"))
+    kl.native.set_option("resume_min", 40)
+    for f in frames[1:]:
+        np.testing.assert_array_equal(frames[0], f)
+    with pytest.raises(_native.NativeError, match="resume_min"):
+        kl.native.set_option("resume_min", 65)
+
+
 def test_wave_counters_are_consistent(kl):
     sc, cam, env, npix, spp, mb, ibl = W.PARITY_CASES["cornell_64_s4"].inputs()
     _launch(kl, sc, cam, env, npix, spp, mb, ibl, "fast")
