@@ -91,6 +91,8 @@ def main():
     ap.add_argument("--bvh", default="sah", choices=["sah", "reference"])
     ap.add_argument("--block", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--check", action="store_true",
+                    help="N>1: rank 0 re-renders the whole frame alone and compares it with the gathered one")
     args = ap.parse_args()
 
     import torch
@@ -103,9 +105,18 @@ def main():
     if world != args.gpus and "WORLD_SIZE" in os.environ:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
     world = max(world, 1)
+    # Rehearsal of the N>1 path on a one-GPU box: every rank on device 0 and the collectives over gloo
+    # on host copies (RCCL refuses two ranks on one GPU).  Never used for measured runs.
+    rehearsal = os.environ.get("BENCH_SAME_DEVICE") == "1"
+    if rehearsal:
+        local = 0
     torch.cuda.set_device(local)
     if world > 1:
-        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", local))
+        if rehearsal:
+            dist.init_process_group("gloo", rank=rank, world_size=world)
+        else:
+            dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", local))
+    coll = "cpu" if rehearsal else "cuda"   # where collective buffers live
 
     wl = Wk.CONFIGS[args.config]
     scene, cam, env, npix, spp, mb, ibl = wl.inputs()
@@ -120,8 +131,9 @@ def main():
     stream = torch.cuda.current_stream()
     mrows = D.max_tile_rows(npix, width, world)
     tile = torch.zeros(3 * width * mrows, dtype=torch.float32, device="cuda")
-    bufs = [torch.empty_like(tile) for _ in range(world)] if (world > 1 and rank == 0) else None
-    frame = torch.empty(3 * npix, dtype=torch.float32, device="cuda") if (rank == 0 and world > 1) else None
+    bufs = [torch.empty(tile.numel(), dtype=torch.float32, device=coll) for _ in range(world)] \
+        if (world > 1 and rank == 0) else None
+    frame = torch.empty(3 * npix, dtype=torch.float32, device=coll) if (rank == 0 and world > 1) else None
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
 
     def step(i=None):
@@ -131,7 +143,7 @@ def main():
         if i is not None:
             ev[i][1].record(stream)
         if world > 1:
-            dist.gather(tile, gather_list=bufs, dst=0)
+            dist.gather(tile if coll == "cuda" else tile.cpu(), gather_list=bufs, dst=0)
             if rank == 0:
                 D.assemble(bufs, width, npix, world, out=frame)
 
@@ -151,20 +163,36 @@ def main():
     elapsed = t1 - t0
     kernel_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
     if world > 1:
-        tt = torch.tensor([elapsed, kernel_ms], dtype=torch.float64, device="cuda")
+        tt = torch.tensor([elapsed, kernel_ms], dtype=torch.float64, device=coll)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed, kernel_ms = float(tt[0]), float(tt[1])
 
     # algorithmic bytes of one launch on this rank: counters of the same traversal x bytes per unit
+    # The bytes are those of the tree walk (FAST over the SAH BVH2): scenes of <= 64 triangles run the
+    # lock-step brute-force path instead, which reads every triangle record per ray from the scalar
+    # cache -- more bytes by construction, so it is not what the roofline is priced on.
+    ctx.set_option("brute_max", 0)
     cnt = ctx.count_work(cam, env, npix, spp, mb, rank, world)
+    ctx.set_option("brute_max", 64)
     wb = ctx.work_bytes()
     alg_bytes = (cnt["node_fetches"] * wb["node_fetch"] + cnt["tri_tests"] * wb["tri_test"]
                  + cnt["rays"] * wb["ray"] + cnt["env_lookups"] * wb["env_lookup"]
                  + D.tile_rows(npix, width, rank, world) * width * 12)   # + the tile written
     if world > 1:
-        tb = torch.tensor([alg_bytes], dtype=torch.float64, device="cuda")
+        tb = torch.tensor([alg_bytes], dtype=torch.float64, device=coll)
         dist.all_reduce(tb, op=dist.ReduceOp.MAX)
         alg_bytes = float(tb[0])
+
+    frame_check = None
+    if args.check and world > 1:
+        step()
+        torch.cuda.synchronize()
+        if rank == 0:
+            full = torch.empty(3 * npix, dtype=torch.float32, device="cuda")
+            ctx.render_device(cam, env, npix, spp, mb, 0, 1, full.data_ptr(), stream.cuda_stream)
+            torch.cuda.synchronize()
+            frame_check = "bit-identical" if torch.equal(full.to(coll), frame) else "MISMATCH"
+        dist.barrier()
 
     if rank == 0:
         samples = npix * spp
@@ -178,12 +206,17 @@ def main():
             "data": wl.data_note(),
             "config": {"workload": wl.name, "scene": wl.scene, "width": wl.width, "height": wl.height,
                        "spp": spp, "max_bounce": mb, "traversal": args.traversal, "bvh": args.bvh,
-                       "parallelism": f"row-interleaved x{world}" + (" + RCCL gather" if world > 1 else "")},
+                       "parallelism": f"row-interleaved x{world}" + (
+                           (" + gloo gather (one-GPU rehearsal)" if rehearsal else " + RCCL gather") if world > 1 else "")},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": _pmc_traffic(wl.name),
                          "kernel_ms": round(kernel_ms, 4), "alg_bytes_per_launch": int(alg_bytes),
+                         "bytes_model": "SURVEY 8(d): 32 B/box tested (FAST node = 2 boxes), 36 B/triangle test, "
+                                        "40 B/ray hit record, 16 B/IBL lookup; counts of this build's SAH tree walk",
                          "counts_per_sample": {k: round(v / (samples / world), 4) for k, v in cnt.items()}},
         }
+        if frame_check is not None:
+            line["frame_check"] = f"gathered {world}-rank frame vs one-device render: {frame_check}"
         if world == 1:
             # the drop-in boundary's own rate: blocking rt_render into host memory (kernel + PCIe read-back)
             host = np.zeros(3 * npix, np.float32)
