@@ -530,6 +530,25 @@ __device__ __forceinline__ void log_event(const FrameParams& F, float kind, int 
     *F.log_count = n + 1;
 }
 
+// Mean + clamp of one pixel (Raytracing.cl:211-220).  RT_NT_STORE: write the
+// frame with nontemporal stores (it is written once and never re-read).
+#ifndef RT_NT_STORE
+#define RT_NT_STORE 0
+#endif
+__device__ __forceinline__ void store_pixel(float* __restrict__ out, int p, rtm_f3 acc, int spp) {
+    const rtm_f3 o = rtm_div(acc, (float)spp);
+    float* dst = out + 3 * (int64_t)p;
+#if RT_NT_STORE
+    __builtin_nontemporal_store(rtm_fmax(rtm_fmin(o.x, 1.0f), 0.0f), dst);
+    __builtin_nontemporal_store(rtm_fmax(rtm_fmin(o.y, 1.0f), 0.0f), dst + 1);
+    __builtin_nontemporal_store(rtm_fmax(rtm_fmin(o.z, 1.0f), 0.0f), dst + 2);
+#else
+    dst[0] = rtm_fmax(rtm_fmin(o.x, 1.0f), 0.0f);
+    dst[1] = rtm_fmax(rtm_fmin(o.y, 1.0f), 0.0f);
+    dst[2] = rtm_fmax(rtm_fmin(o.z, 1.0f), 0.0f);
+#endif
+}
+
 enum Phase { FETCH = 0, PRIMARY = 1, PREP = 2, BOUNCE = 3, SUN = 4, DONE = 5 };
 
 // RT_MIN_WAVES: waves per SIMD the register allocator must leave room for (0 = compiler's choice).
@@ -680,11 +699,7 @@ __global__ void RT_RENDER_BOUNDS render_kernel(DevScene S, FrameParams F, float*
                     so = rtm_v3(1, 1, 1);
                 }
                 if (phase == FETCH) {
-                    const rtm_f3 o = rtm_div(acc, (float)spp);
-                    float* dst = out + 3 * (int64_t)p;
-                    dst[0] = rtm_fmax(rtm_fmin(o.x, 1.0f), 0.0f);
-                    dst[1] = rtm_fmax(rtm_fmin(o.y, 1.0f), 0.0f);
-                    dst[2] = rtm_fmax(rtm_fmin(o.z, 1.0f), 0.0f);
+                    store_pixel(out, p, acc, spp);
                 }
                 continue;
             }
@@ -702,11 +717,7 @@ __global__ void RT_RENDER_BOUNDS render_kernel(DevScene S, FrameParams F, float*
             so = rtm_v3(1, 1, 1);
             phase = PREP;
             if (spp <= 0) {   // reference: output = 0/0 -> NaN -> clamp gives 1
-                const rtm_f3 o = rtm_div(acc, (float)spp);
-                float* dst = out + 3 * (int64_t)p;
-                dst[0] = rtm_fmax(rtm_fmin(o.x, 1.0f), 0.0f);
-                dst[1] = rtm_fmax(rtm_fmin(o.y, 1.0f), 0.0f);
-                dst[2] = rtm_fmax(rtm_fmin(o.z, 1.0f), 0.0f);
+                store_pixel(out, p, acc, spp);
                 phase = FETCH;
             }
             continue;
@@ -751,11 +762,7 @@ __global__ void RT_RENDER_BOUNDS render_kernel(DevScene S, FrameParams F, float*
             acc = rtm_add(acc, so);
             ++s;
             if (s >= spp) {
-                const rtm_f3 o = rtm_div(acc, (float)spp);
-                float* dst = out + 3 * (int64_t)p;
-                dst[0] = rtm_fmax(rtm_fmin(o.x, 1.0f), 0.0f);
-                dst[1] = rtm_fmax(rtm_fmin(o.y, 1.0f), 0.0f);
-                dst[2] = rtm_fmax(rtm_fmin(o.z, 1.0f), 0.0f);
+                store_pixel(out, p, acc, spp);
                 phase = FETCH;
             } else {
                 Ro = C.position; Rd = cd; tri = tc; k = kc; j = 0;
@@ -917,27 +924,22 @@ __global__ void RT_RENDER_BOUNDS render_resume_kernel(DevScene S, FrameParams F,
     rtm_f3 acc = rtm_v3(0, 0, 0);
     int s = 0;
 
-    auto write_pixel = [&]() {
-        const rtm_f3 o = rtm_div(acc, (float)spp);   // mean + clamp, Raytracing.cl:211-220
-        float* dst = out + 3 * (int64_t)p;
-        dst[0] = rtm_fmax(rtm_fmin(o.x, 1.0f), 0.0f);
-        dst[1] = rtm_fmax(rtm_fmin(o.y, 1.0f), 0.0f);
-        dst[2] = rtm_fmax(rtm_fmin(o.z, 1.0f), 0.0f);
+    auto write_pixel = [&]() __attribute__((always_inline)) {
+        store_pixel(out, p, acc, spp);
     };
-    auto finish_sample = [&]() {  // output += baseColor; next sample from the cached camera hit
+    auto finish_sample = [&]() __attribute__((always_inline)) {  // output += baseColor; next sample from the cached camera hit
         if (LOG && logme) log_event(F, 3.0f, s + 1, rtm_v3(0, 0, 0), rtm_v3(0, 0, 0), 0.0f, 0, so);
         acc = rtm_add(acc, so);
         ++s;
-        if (s >= spp) {
-            write_pixel();
-            phase = FETCH;
-        } else {
-            Ro = C.position; Rd = cd; tri = tc; k = kc; j = 0;
-            so = rtm_v3(1, 1, 1);
-            phase = PREP;
-        }
+        if (s >= spp) write_pixel();
+        // the next sample restarts from the cached camera hit; written as selects so that no branch
+        // ends in a store the compiler could merge with the pixel store (that would force the path
+        // state into scratch memory through a generic pointer)
+        phase = s >= spp ? FETCH : PREP;
+        Ro = C.position; Rd = cd; tri = tc; k = kc; j = 0;
+        so = rtm_v3(1, 1, 1);
     };
-    auto start = [&](rtm_f3 o, rtm_f3 d) {
+    auto start = [&](rtm_f3 o, rtm_f3 d) __attribute__((always_inline)) {
         tracing = !fast_init<COUNT>(S, T, o, d, c);
     };
 

@@ -1,12 +1,12 @@
 """Print per-launch PMC values of the render kernel from tools/run_diag.sh output."""
-import csv, glob, sys, collections
+import csv, glob, re, sys, collections
 import numpy as np
 prof = sys.argv[1]
-kern = sys.argv[2] if len(sys.argv) > 2 else "render_kernel<0, false, false"
+kern = sys.argv[2] if len(sys.argv) > 2 else r"render(_resume)?_kernel<(0, )?false, false"
 vals = collections.defaultdict(list)
 for p in glob.glob(prof + "/*/*counter_collection.csv"):
     for r in csv.DictReader(open(p, newline="")):
-        if kern in r["Kernel_Name"]:
+        if re.search(kern, r["Kernel_Name"]):
             vals[r["Counter_Name"]].append(float(r["Counter_Value"]))
 v = {k: float(np.mean(x)) for k, x in vals.items()}
 for k in sorted(v):

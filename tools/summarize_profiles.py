@@ -8,6 +8,7 @@ bytes per launch, corrected as MI355X_MICROARCH.md prescribes for gfx950 (FETCH_
 KiB and reads 1/2 of a wide streaming read's bytes -> x2; WRITE_SIZE in KiB, exact).
 """
 import csv
+import re
 import glob
 import json
 import os
@@ -17,7 +18,7 @@ import sys
 import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-KERNEL = "render_kernel<0, false, false"  # FAST, uninstrumented (any SMEM variant)
+KERNEL = r"render(_resume)?_kernel<(0, )?false, false"  # FAST, uninstrumented (any variant)
 
 
 def _rows(pattern):
@@ -35,13 +36,13 @@ def main(prof, tag, workload, kernel=KERNEL):
     if stats:
         shutil.copy(stats[0], os.path.join(ROOT, "profiles", f"{tag}_kernel_stats_{workload}.csv"))
         for r in _rows(stats[0]):
-            if kernel in r["Name"]:
+            if re.search(kernel, r["Name"]):
                 summary["kernel_calls"] = int(r["Calls"])
                 summary["kernel_avg_ms"] = float(r["AverageNs"]) / 1e6
     counters = {}
     for sub in ("fetch", "write", "dram"):
         for r in _rows(os.path.join(prof, sub, "*counter_collection.csv")):
-            if kernel in r["Kernel_Name"]:
+            if re.search(kernel, r["Kernel_Name"]):
                 counters.setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))
     for k, v in counters.items():
         summary[k + "_per_launch"] = float(np.mean(v))
