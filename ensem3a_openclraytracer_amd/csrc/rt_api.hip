@@ -42,6 +42,8 @@ struct DevBuf {
 struct Device {
     int id = 0;
     hipStream_t stream = nullptr;
+    int cus = 0;                  // compute units (sizes the FAST stack overflow buffer)
+    DevBuf stack_ovf;             // FAST traversal stack entries beyond the LDS part
     DevBuf nodes, brute, bvh9, tri_geo, tri_shade, tri_frame, mat, ibl, out, counts, work, scratch_a, scratch_b;
     float* host_stage = nullptr;  // pinned staging for rt_render
     size_t host_stage_bytes = 0;
@@ -297,12 +299,22 @@ void pack_checked(HostScene& hs, const float* bvh9, int64_t nb, int64_t ntri, in
     hs.fast_ok = (ntri > 0) ? pack_fast(hs, bvh9, nb, ntri, layout, brute_max, why) : true;
     if (ntri == 0) { hs.nnodes = 0; hs.root_ref = 0; hs.depth = 1; hs.nodes.clear(); hs.brute.clear(); hs.nbrute = 0; }
     if (!hs.fast_ok) { hs.brute.clear(); hs.nbrute = 0; }
-    if (hs.fast_ok && (int64_t)hs.depth * 256 * 8 > 64 * 1024) {  // int2 stack entries, block <= 256
+    // render kernels keep kStackLds entries in LDS and spill deeper ones to HBM; the single-ray
+    // debug kernel keeps the whole stack in LDS (int2 entries, 128 lanes): depth <= 64
+    if (hs.fast_ok && hs.depth > 64) {
         hs.fast_ok = false;
-        why = "tree too deep for the LDS stack";
+        why = "tree deeper than 64 levels";
     }
     if (hs.nodes.empty()) hs.nodes.assign(16, 0.0f);
     if (hs.brute.empty()) hs.brute.assign(16, 0.0f);
+}
+
+// HBM part of the FAST traversal stack: (depth - kStackLds) entries for every lane a
+// persistent render grid can hold.
+hipError_t ensure_stack_ovf(Device& d, const HostScene& hs) {
+    const int64_t extra = (int64_t)hs.depth - rt::kStackLds;
+    if (extra <= 0) return hipSuccess;
+    return ensure(d.stack_ovf, (size_t)std::max(d.cus, 1) * rt::kMaxLanesPerCu * (size_t)extra * sizeof(int2));
 }
 
 template <typename T>
@@ -333,6 +345,8 @@ rt::DevScene dev_scene(const rt_ctx* ctx, const Device& d) {
     s.depth = ctx->hs.depth;
     s.brute = (const float4*)d.brute.p;
     s.nbrute = ctx->hs.nbrute;
+    s.stack_lds = std::min<int32_t>(ctx->hs.depth > 0 ? ctx->hs.depth : 1, rt::kStackLds);
+    s.stack_ovf = (int2*)d.stack_ovf.p;
     return s;
 }
 
@@ -396,8 +410,9 @@ int rt_create(int n_devices, const int* device_ids, rt_ctx** out) {
             return set_err(nullptr, RT_ERR_ARG, "device id %d out of range", id);
         }
         ctx->devs[i].id = id;
-        if ((e = hipSetDevice(id)) != hipSuccess || (e = hipStreamCreateWithFlags(&ctx->devs[i].stream,
-                                                                                 hipStreamNonBlocking)) != hipSuccess) {
+        if ((e = hipSetDevice(id)) != hipSuccess ||
+            (e = hipStreamCreateWithFlags(&ctx->devs[i].stream, hipStreamNonBlocking)) != hipSuccess ||
+            (e = hipDeviceGetAttribute(&ctx->devs[i].cus, hipDeviceAttributeMultiprocessorCount, id)) != hipSuccess) {
             rt_destroy(ctx);
             return set_err(nullptr, RT_ERR_HIP, "device %d init failed: %s", id, hipGetErrorString(e));
         }
@@ -411,7 +426,7 @@ void rt_destroy(rt_ctx* ctx) {
     for (auto& d : ctx->devs) {
         if (hipSetDevice(d.id) != hipSuccess) continue;
         if (d.stream) (void)hipStreamSynchronize(d.stream);
-        for (DevBuf* b : {&d.nodes, &d.brute, &d.bvh9, &d.tri_geo, &d.tri_shade, &d.tri_frame, &d.mat, &d.ibl, &d.out,
+        for (DevBuf* b : {&d.stack_ovf, &d.nodes, &d.brute, &d.bvh9, &d.tri_geo, &d.tri_shade, &d.tri_frame, &d.mat, &d.ibl, &d.out,
                           &d.counts, &d.work, &d.scratch_a, &d.scratch_b})
             release(*b);
         if (d.host_stage) (void)hipHostFree(d.host_stage);
@@ -448,6 +463,7 @@ int rt_set_option(rt_ctx* ctx, const char* key, int64_t value) {
             HIP_OR_RET(ctx, upload(d.nodes, hs.nodes, d.stream));
             HIP_OR_RET(ctx, upload(d.brute, hs.brute, d.stream));
             HIP_OR_RET(ctx, upload(d.tri_geo, hs.tri_geo, d.stream));
+            HIP_OR_RET(ctx, ensure_stack_ovf(d, hs));
             HIP_OR_RET(ctx, hipStreamSynchronize(d.stream));
         }
         if (!hs.fast_ok) ctx->err = "FAST traversal unavailable (" + why + "); REF traversal will be used";
@@ -550,6 +566,7 @@ int rt_set_scene(rt_ctx* ctx, const float* vp, int64_t nvp, const float* vn, int
         HIP_OR_RET(ctx, hipSetDevice(d.id));
         HIP_OR_RET(ctx, upload(d.nodes, hs.nodes, d.stream));
         HIP_OR_RET(ctx, upload(d.brute, hs.brute, d.stream));
+        HIP_OR_RET(ctx, ensure_stack_ovf(d, hs));
         HIP_OR_RET(ctx, upload(d.bvh9, hs.bvh9, d.stream));
         HIP_OR_RET(ctx, upload(d.tri_geo, hs.tri_geo, d.stream));
         HIP_OR_RET(ctx, upload(d.tri_shade, hs.tri_shade, d.stream));

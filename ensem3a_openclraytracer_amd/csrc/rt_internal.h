@@ -6,6 +6,13 @@
 
 namespace rt {
 
+// LDS entries of the FAST traversal stack per lane (int2 each); deeper entries spill to HBM.
+#ifndef RT_STACK_LDS
+#define RT_STACK_LDS 20
+#endif
+constexpr int kStackLds = RT_STACK_LDS;
+constexpr int kMaxLanesPerCu = 2048;   // resident threads per CU (gfx950)
+
 // Device view of one uploaded scene (all pointers are device pointers).
 struct DevScene {
     // FAST traversal: BVH2 nodes holding both child boxes, 4 x float4 each:
@@ -34,6 +41,10 @@ struct DevScene {
     const uchar4* ibl;
     int32_t ibl_w, ibl_h;
     int32_t depth;         // max number of FAST stack entries a ray can need
+    // FAST traversal stack: the first stack_lds entries of each lane in LDS, deeper ones
+    // (rare) in stack_ovf, a device buffer of (depth - stack_lds) x resident lanes int2 entries
+    int32_t stack_lds;
+    int2* stack_ovf;
     // FAST on small scenes: one 64-byte record per reachable triangle in reference DFS order
     // (leaf box, a.p, e1, e2, triangle index); nbrute = 0 when the BVH path is used
     const float4* brute;

@@ -189,22 +189,58 @@ __device__ __forceinline__ bool mt_flat(const char* __restrict__ tb, unsigned to
     return !parallel && !(u < 0.0f || u > 1.0f) && !(v < 0.0f || u + v > 1.0f) && (k > 0.0000001f);
 }
 
+// A lane's FAST traversal stack: entries below cap bytes in LDS ([entry][blockDim]
+// int2, conflict-free), deeper ones in the HBM overflow buffer ([entry][lanes]).
+// off = entry index * stride (bytes of LDS between a lane's entries).
+struct LaneStack {
+    char* lds;                       // per lane
+    int2* ovf;                       // uniform base; the lane's slot is added only on the rare spill path
+    unsigned stride, cap, shift, ostride;
+    __device__ __forceinline__ unsigned slot(unsigned off) const {
+        return ((off - cap) >> shift) * ostride + blockIdx.x * blockDim.x + threadIdx.x;
+    }
+    // OVF = false: the whole stack fits in LDS (stack_lds == depth) and no spill code is emitted
+    template <bool OVF>
+    __device__ __forceinline__ void put(unsigned off, int2 e) const {
+        if (!OVF || off < cap) *reinterpret_cast<int2*>(lds + off) = e;
+        else ovf[slot(off)] = e;
+    }
+    template <bool OVF>
+    __device__ __forceinline__ int2 get(unsigned off) const {
+        int2 e;
+        if (!OVF || off < cap) e = *reinterpret_cast<const int2*>(lds + off);
+        else e = ovf[slot(off)];
+        return e;
+    }
+};
+
+__device__ __forceinline__ LaneStack lane_stack(const DevScene& S, int* lds_base) {
+    LaneStack st;
+    const unsigned B = blockDim.x;
+    st.lds = reinterpret_cast<char*>(lds_base) + 8 * threadIdx.x;
+    st.stride = 8u * B;
+    st.cap = (unsigned)S.stack_lds * st.stride;
+    st.shift = (unsigned)__builtin_ctz(st.stride);
+    st.ovf = S.stack_ovf;
+    st.ostride = gridDim.x * B;
+    return st;
+}
+
 // One item per iteration: an internal node (both child boxes tested, nearer hit
 // child continues, the farther is pushed with its entry distance) or a leaf
 // (one triangle test).  Popped items whose entry distance is beyond the best hit
 // are discarded without a fetch.  Stack entries: int2 (ref, tmin bits) in LDS.
-template <bool COUNT, bool SOA>
+template <bool COUNT, bool SOA, bool OVF>
 __device__ Hit trace_fast(const DevScene& S, const float4* __restrict__ nodes, const float4* __restrict__ tris,
-                          rtm_f3 o, rtm_f3 d, int* __restrict__ stk_base, int B, Cnt& c) {
+                          rtm_f3 o, rtm_f3 d, const LaneStack& st, Cnt& c) {
     Hit best{1000.0f, -1};
     int best_rank = -1;
     if (COUNT) c.rays++;
     if (S.ntri <= 0) return best;
-    // Stack entries int2 (ref, tmin bits) at [depth][B] in LDS, addressed by a running byte offset
-    // (push: += 8B, pop: -= 8B), node and triangle records by 32-bit byte offsets: the loop has no
-    // integer multiplies.
-    char* const sb = reinterpret_cast<char*>(stk_base - threadIdx.x) + 8 * threadIdx.x;
-    const unsigned sstride = 8u * (unsigned)B;
+    // Stack entries int2 (ref, tmin bits) addressed by a running byte offset (push: += stride,
+    // pop: -= stride), node and triangle records by 32-bit byte offsets: the loop has no integer
+    // multiplies.
+    const unsigned sstride = st.stride;
     const char* const nb = reinterpret_cast<const char*>(nodes);
     const char* const tb = reinterpret_cast<const char*>(tris);
     // AoS: node i = 64 bytes at 64 i; SOA (LDS copy): plane k of node i at 16 (k nnodes + i), so
@@ -241,7 +277,7 @@ __device__ Hit trace_fast(const DevScene& S, const float4* __restrict__ nodes, c
 #endif
             if (h0 && h1) {
                 const bool first0 = t0n <= t1n;
-                *reinterpret_cast<int2*>(sb + soff) = make_int2(first0 ? e.y : e.x, __float_as_int(first0 ? t1n : t0n));
+                st.template put<OVF>(soff, make_int2(first0 ? e.y : e.x, __float_as_int(first0 ? t1n : t0n)));
                 soff += sstride;
                 item = first0 ? e.x : e.y;
                 continue;
@@ -266,7 +302,7 @@ __device__ Hit trace_fast(const DevScene& S, const float4* __restrict__ nodes, c
         item = 0x7fffffff;
         while (soff > 0) {
             soff -= sstride;
-            const int2 en = *reinterpret_cast<const int2*>(sb + soff);
+            const int2 en = st.template get<OVF>(soff);
             if (__int_as_float(en.y) <= best.k * CULL_MARGIN) {
                 item = en.x;
                 break;
@@ -329,12 +365,13 @@ __device__ Hit trace_brute(const DevScene& S, rtm_f3 o, rtm_f3 d, Cnt& c) {
     return best;
 }
 
-template <int TRAV, bool COUNT, bool SOA = false>
+// stk/B: the REF traversal's int stack in LDS; st: the FAST traversal's stack.
+template <int TRAV, bool COUNT, bool SOA = false, bool OVF = false>
 __device__ __forceinline__ Hit trace(const DevScene& S, const float4* nodes, const float4* tris, rtm_f3 o, rtm_f3 d,
-                                     int* stk, int B, Cnt& c) {
+                                     int* stk, int B, const LaneStack& st, Cnt& c) {
     if (TRAV == TRAV_REF) return trace_ref<COUNT>(S, o, d, stk, B, c);
     if (S.nbrute > 0) return trace_brute<COUNT>(S, o, d, c);
-    return trace_fast<COUNT, SOA>(S, nodes, tris, o, d, stk, B, c);
+    return trace_fast<COUNT, SOA, OVF>(S, nodes, tris, o, d, st, c);
 }
 
 // ---- per-launch constants (Raytracing.cl:18-37, 115-118; MathLib.cl:72-80) ----
@@ -567,7 +604,7 @@ enum Phase { FETCH = 0, PRIMARY = 1, PREP = 2, BOUNCE = 3, SUN = 4, DONE = 5 };
 // base + (its rank among the requesting lanes) -- so no lane idles while the
 // rest of its wave finishes a slower pixel.  Per loop iteration every busy
 // lane traces exactly one ray (primary, bounce or sun ray).
-template <int TRAV, bool COUNT, bool LOG = false, bool SMEM = false>
+template <int TRAV, bool COUNT, bool LOG = false, bool SMEM = false, bool OVF = false>
 __global__ void RT_RENDER_BOUNDS render_kernel(DevScene S, FrameParams F, float* __restrict__ out,
                                                unsigned long long* __restrict__ counts,
                                                unsigned int* __restrict__ work_counter,
@@ -575,6 +612,7 @@ __global__ void RT_RENDER_BOUNDS render_kernel(DevScene S, FrameParams F, float*
     extern __shared__ int lds_stack[];
     const int B = blockDim.x;
     int* stk = lds_stack + threadIdx.x;
+    const LaneStack lst = lane_stack(S, lds_stack);
     Cnt c{0, 0, 0, 0, 0, 0, 0};
     const LaunchConst& C = *lconst;   // uniform: scalar loads, no VGPRs
     // SMEM: the whole BVH2 node array and triangle array of a small scene are
@@ -582,7 +620,7 @@ __global__ void RT_RENDER_BOUNDS render_kernel(DevScene S, FrameParams F, float*
     const float4* nodes = S.nodes;
     const float4* tris = S.tri_geo;
     if (SMEM) {
-        float4* ln = reinterpret_cast<float4*>(lds_stack + 2 * S.depth * B);
+        float4* ln = reinterpret_cast<float4*>(lds_stack + 2 * S.stack_lds * B);
         float4* lt = ln + 4 * S.nnodes;
         for (int q = threadIdx.x; q < 4 * S.nnodes; q += B) ln[(q & 3) * S.nnodes + (q >> 2)] = S.nodes[q];
         for (int q = threadIdx.x; q < 3 * S.ntri; q += B) lt[q] = S.tri_geo[q];
@@ -708,7 +746,7 @@ __global__ void RT_RENDER_BOUNDS render_kernel(DevScene S, FrameParams F, float*
         // -- one ray per busy lane --
         const rtm_f3 to = (phase == PRIMARY) ? C.position : Bo;
         const rtm_f3 td = (phase == PRIMARY) ? cd : ((phase == BOUNCE) ? Bd : C.sun);
-        const Hit h = trace<TRAV, COUNT, SMEM>(S, nodes, tris, to, td, stk, B, c);
+        const Hit h = trace<TRAV, COUNT, SMEM, OVF>(S, nodes, tris, to, td, stk, B, lst, c);
         bool finish = false;
         if (phase == PRIMARY) {
             tc = h.tri;
@@ -823,9 +861,10 @@ __device__ __forceinline__ bool fast_init(const DevScene& S, FastRay& R, rtm_f3 
 // One round of trace_fast's loop: descend nearest children until a leaf is
 // tested or nothing is hit, then pop the next live stack entry.  Same
 // arithmetic and order as trace_fast.  Returns true when the ray is finished.
-template <bool COUNT, bool SOA>
-__device__ __forceinline__ bool fast_round(const DevScene& S, FastRay& R, const char* nb, const char* tb, char* sb,
-                                           unsigned sstride, unsigned kstride, Cnt& c) {
+template <bool COUNT, bool SOA, bool OVF>
+__device__ __forceinline__ bool fast_round(const DevScene& S, FastRay& R, const char* nb, const char* tb,
+                                           const LaneStack& st, unsigned kstride, Cnt& c) {
+    const unsigned sstride = st.stride;
     const float oix = R.o.x * R.ix, oiy = R.o.y * R.iy, oiz = R.o.z * R.iz;
     while (R.item >= 0) {
         if (COUNT) { count_wave(c.wave_trav); c.nodes++; }
@@ -842,7 +881,7 @@ __device__ __forceinline__ bool fast_round(const DevScene& S, FastRay& R, const 
         const bool h1 = fmaxf(t1n, 0.0f) <= fminf(t1x, cull);
         if (h0 && h1) {
             const bool first0 = t0n <= t1n;
-            *reinterpret_cast<int2*>(sb + R.soff) = make_int2(first0 ? e.y : e.x, __float_as_int(first0 ? t1n : t0n));
+            st.template put<OVF>(R.soff, make_int2(first0 ? e.y : e.x, __float_as_int(first0 ? t1n : t0n)));
             R.soff += sstride;
             R.item = first0 ? e.x : e.y;
         } else if (h0 || h1) {
@@ -865,7 +904,7 @@ __device__ __forceinline__ bool fast_round(const DevScene& S, FastRay& R, const 
     }
     while (R.soff > 0) {   // pop the next item still in front of the best hit
         R.soff -= sstride;
-        const int2 en = *reinterpret_cast<const int2*>(sb + R.soff);
+        const int2 en = st.template get<OVF>(R.soff);
         if (__int_as_float(en.y) <= R.bk * CULL_MARGIN) {
             R.item = en.x;
             return false;
@@ -874,8 +913,17 @@ __device__ __forceinline__ bool fast_round(const DevScene& S, FastRay& R, const 
     return true;
 }
 
-template <bool COUNT, bool LOG, bool SMEM>
-__global__ void RT_RENDER_BOUNDS render_resume_kernel(DevScene S, FrameParams F, float* __restrict__ out,
+#ifndef RT_RESUME_MIN_WAVES
+#define RT_RESUME_MIN_WAVES 0
+#endif
+#if RT_RESUME_MIN_WAVES > 0
+#define RT_RESUME_BOUNDS __launch_bounds__(256, RT_RESUME_MIN_WAVES)
+#else
+#define RT_RESUME_BOUNDS __launch_bounds__(256)
+#endif
+
+template <bool COUNT, bool LOG, bool SMEM, bool OVF>
+__global__ void RT_RESUME_BOUNDS render_resume_kernel(DevScene S, FrameParams F, float* __restrict__ out,
                                                       unsigned long long* __restrict__ counts,
                                                       unsigned int* __restrict__ work_counter,
                                                       const LaunchConst* __restrict__ lconst) {
@@ -886,7 +934,7 @@ __global__ void RT_RENDER_BOUNDS render_resume_kernel(DevScene S, FrameParams F,
     const float4* nodes = S.nodes;
     const float4* tris = S.tri_geo;
     if (SMEM) {
-        float4* ln = reinterpret_cast<float4*>(lds_stack + 2 * S.depth * B);
+        float4* ln = reinterpret_cast<float4*>(lds_stack + 2 * S.stack_lds * B);
         float4* lt = ln + 4 * S.nnodes;
         for (int q = threadIdx.x; q < 4 * S.nnodes; q += B) ln[(q & 3) * S.nnodes + (q >> 2)] = S.nodes[q];
         for (int q = threadIdx.x; q < 3 * S.ntri; q += B) lt[q] = S.tri_geo[q];
@@ -894,8 +942,7 @@ __global__ void RT_RENDER_BOUNDS render_resume_kernel(DevScene S, FrameParams F,
         nodes = ln;
         tris = lt;
     }
-    char* const sb = reinterpret_cast<char*>(lds_stack) + 8 * threadIdx.x;
-    const unsigned sstride = 8u * (unsigned)B;
+    const LaneStack lst = lane_stack(S, lds_stack);
     const char* const nb = reinterpret_cast<const char*>(nodes);
     const char* const tb = reinterpret_cast<const char*>(tris);
     const unsigned kstride = SMEM ? 16u * (unsigned)S.nnodes : 16u;
@@ -1080,7 +1127,7 @@ __global__ void RT_RENDER_BOUNDS render_resume_kernel(DevScene S, FrameParams F,
 
         // -- traversal rounds until at least F.resume_min lanes have no ray in flight --
         while (true) {
-            if (tracing && fast_round<COUNT, SMEM>(S, T, nb, tb, sb, sstride, kstride, c)) tracing = false;
+            if (tracing && fast_round<COUNT, SMEM, OVF>(S, T, nb, tb, lst, kstride, c)) tracing = false;
             const unsigned long long tr = __ballot(tracing);
             if (tr == 0 || 64 - __popcll(tr) >= F.resume_min) break;
         }
@@ -1104,11 +1151,11 @@ __global__ void gamma_kernel(const float* __restrict__ in, float* __restrict__ o
     }
 }
 
-template <int TRAV, bool COUNT, bool LOG, bool SMEM = false, bool RESUME = false>
+template <int TRAV, bool COUNT, bool LOG, bool SMEM = false, bool RESUME = false, bool OVF = false>
 hipError_t launch_t(const DevScene& sc, const FrameParams& fp, int block, float* d_out, unsigned long long* d_counts,
                     unsigned int* d_work, hipStream_t stream) {
     // FAST: int2 entries; the brute-force path of small scenes needs no stack
-    const int depth = (TRAV == TRAV_REF) ? REF_STACK : (sc.nbrute > 0 ? 1 : 2 * (sc.depth > 0 ? sc.depth : 1));
+    const int depth = (TRAV == TRAV_REF) ? REF_STACK : (sc.nbrute > 0 ? 1 : 2 * (sc.stack_lds > 0 ? sc.stack_lds : 1));
     size_t lds = (size_t)depth * block * sizeof(int);
     if (SMEM) lds += (size_t)(4 * sc.nnodes + 3 * sc.ntri) * sizeof(float4);
     const int64_t need = (fp.nloc + block - 1) / block;
@@ -1117,8 +1164,8 @@ hipError_t launch_t(const DevScene& sc, const FrameParams& fp, int block, float*
     int dev = 0, cus = 0, per_cu = 0;
     hipError_t e = hipGetDevice(&dev);
     if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    const void* kfn = RESUME ? (const void*)render_resume_kernel<COUNT, LOG, SMEM>
-                             : (const void*)render_kernel<TRAV, COUNT, LOG, SMEM>;
+    const void* kfn = RESUME ? (const void*)render_resume_kernel<COUNT, LOG, SMEM, OVF>
+                             : (const void*)render_kernel<TRAV, COUNT, LOG, SMEM, OVF>;
     if (e == hipSuccess) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kfn, block, lds);
     if (e != hipSuccess) return e;
     const int64_t resident = (int64_t)std::max(1, cus) * std::max(1, per_cu);
@@ -1129,10 +1176,10 @@ hipError_t launch_t(const DevScene& sc, const FrameParams& fp, int block, float*
     LaunchConst* lc = reinterpret_cast<LaunchConst*>(reinterpret_cast<char*>(d_work) + 64);
     hipLaunchKernelGGL(make_const_kernel, dim3(1), dim3(64), 0, stream, fp, lc);
     if (RESUME)
-        hipLaunchKernelGGL((render_resume_kernel<COUNT, LOG, SMEM>), dim3((unsigned)grid), dim3(block), lds, stream,
+        hipLaunchKernelGGL((render_resume_kernel<COUNT, LOG, SMEM, OVF>), dim3((unsigned)grid), dim3(block), lds, stream,
                            sc, fp, d_out, d_counts, d_work, (const LaunchConst*)lc);
     else
-        hipLaunchKernelGGL((render_kernel<TRAV, COUNT, LOG, SMEM>), dim3((unsigned)grid), dim3(block), lds, stream,
+        hipLaunchKernelGGL((render_kernel<TRAV, COUNT, LOG, SMEM, OVF>), dim3((unsigned)grid), dim3(block), lds, stream,
                            sc, fp, d_out, d_counts, d_work, (const LaunchConst*)lc);
     return hipGetLastError();
 }
@@ -1167,7 +1214,7 @@ __global__ void __launch_bounds__(256) debug_trace_kernel(DevScene S, const floa
     Cnt c{0, 0, 0, 0, 0, 0, 0};
     const float* r = rays + 6 * t;
     const Hit h = trace<TRAV, false>(S, S.nodes, S.tri_geo, rtm_v3(r[3], r[4], r[5]), rtm_v3(r[0], r[1], r[2]),
-                                     lds_stack + threadIdx.x, blockDim.x, c);
+                                     lds_stack + threadIdx.x, blockDim.x, lane_stack(S, lds_stack), c);
     out[2 * t + 0] = h.k;
     out[2 * t + 1] = (float)h.tri;
 }
@@ -1183,6 +1230,8 @@ hipError_t launch_debug_math(int fn, const float* x, const float* y, float* out,
 hipError_t launch_debug_log(const DevScene& sc, const FrameParams& fp, int traversal, float* d_out,
                             unsigned int* d_work, hipStream_t stream) {
     if (traversal == TRAV_REF) return launch_t<TRAV_REF, false, true>(sc, fp, 64, d_out, nullptr, d_work, stream);
+    if (sc.nbrute == 0 && sc.stack_lds < sc.depth)
+        return launch_t<TRAV_FAST, false, true, false, false, true>(sc, fp, 64, d_out, nullptr, d_work, stream);
     return launch_t<TRAV_FAST, false, true>(sc, fp, 64, d_out, nullptr, d_work, stream);
 }
 
@@ -1197,15 +1246,39 @@ hipError_t launch_debug_trace(const DevScene& sc, int traversal, const float* ra
                               hipStream_t stream) {
     if (n <= 0) return hipSuccess;
     const int block = 128;
-    const int depth = traversal == TRAV_REF ? REF_STACK : 2 * (sc.depth > 0 ? sc.depth : 1);
+    // not a persistent grid: the whole FAST stack lives in LDS (no overflow buffer sized for this grid)
+    DevScene s2 = sc;
+    s2.stack_lds = sc.depth > 0 ? sc.depth : 1;
+    s2.stack_ovf = nullptr;
+    const int depth = traversal == TRAV_REF ? REF_STACK : 2 * s2.stack_lds;
     const size_t lds = (size_t)depth * block * sizeof(int);
     if (traversal == TRAV_REF)
         hipLaunchKernelGGL(debug_trace_kernel<TRAV_REF>, dim3((unsigned)((n + block - 1) / block)), dim3(block), lds,
-                           stream, sc, rays, out, n);
+                           stream, s2, rays, out, n);
     else
         hipLaunchKernelGGL(debug_trace_kernel<TRAV_FAST>, dim3((unsigned)((n + block - 1) / block)), dim3(block), lds,
-                           stream, sc, rays, out, n);
+                           stream, s2, rays, out, n);
     return hipGetLastError();
+}
+
+template <bool COUNT>
+hipError_t launch_fast(const DevScene& sc, const FrameParams& fp, int block, float* d_out,
+                       unsigned long long* d_counts, unsigned int* d_work, hipStream_t stream) {
+    const size_t scene_bytes = (size_t)(4 * sc.nnodes + 3 * sc.ntri) * sizeof(float4);
+    const bool smem = sc.ntri > 0 && sc.nbrute == 0 && scene_bytes <= (size_t)RT_LDS_SCENE_MAX;
+    const bool ovf = sc.nbrute == 0 && sc.stack_lds < sc.depth;
+    const bool resume = sc.ntri > 0 && sc.nbrute == 0 && fp.resume_min > 0;
+    if (resume) {
+        if (smem) return launch_t<TRAV_FAST, COUNT, false, true, true>(sc, fp, block, d_out, d_counts, d_work, stream);
+        if (ovf)
+            return launch_t<TRAV_FAST, COUNT, false, false, true, true>(sc, fp, block, d_out, d_counts, d_work,
+                                                                          stream);
+        return launch_t<TRAV_FAST, COUNT, false, false, true>(sc, fp, block, d_out, d_counts, d_work, stream);
+    }
+    if (smem) return launch_t<TRAV_FAST, COUNT, false, true>(sc, fp, block, d_out, d_counts, d_work, stream);
+    if (ovf)
+        return launch_t<TRAV_FAST, COUNT, false, false, false, true>(sc, fp, block, d_out, d_counts, d_work, stream);
+    return launch_t<TRAV_FAST, COUNT, false>(sc, fp, block, d_out, d_counts, d_work, stream);
 }
 
 hipError_t launch_render(const DevScene& sc, const FrameParams& fp, int traversal, int block, float* d_out,
@@ -1214,21 +1287,8 @@ hipError_t launch_render(const DevScene& sc, const FrameParams& fp, int traversa
         return d_counts ? launch_t<TRAV_REF, true, false>(sc, fp, block, d_out, d_counts, d_work, stream)
                         : launch_t<TRAV_REF, false, false>(sc, fp, block, d_out, d_counts, d_work, stream);
     }
-    const size_t scene_bytes = (size_t)(4 * sc.nnodes + 3 * sc.ntri) * sizeof(float4);
-    if (sc.ntri > 0 && sc.nbrute == 0 && fp.resume_min > 0) {
-        if (scene_bytes <= (size_t)RT_LDS_SCENE_MAX)
-            return d_counts ? launch_t<TRAV_FAST, true, false, true, true>(sc, fp, block, d_out, d_counts, d_work, stream)
-                            : launch_t<TRAV_FAST, false, false, true, true>(sc, fp, block, d_out, d_counts, d_work,
-                                                                            stream);
-        return d_counts ? launch_t<TRAV_FAST, true, false, false, true>(sc, fp, block, d_out, d_counts, d_work, stream)
-                        : launch_t<TRAV_FAST, false, false, false, true>(sc, fp, block, d_out, d_counts, d_work, stream);
-    }
-    if (sc.ntri > 0 && sc.nbrute == 0 && scene_bytes <= (size_t)RT_LDS_SCENE_MAX) {
-        return d_counts ? launch_t<TRAV_FAST, true, false, true>(sc, fp, block, d_out, d_counts, d_work, stream)
-                        : launch_t<TRAV_FAST, false, false, true>(sc, fp, block, d_out, d_counts, d_work, stream);
-    }
-    return d_counts ? launch_t<TRAV_FAST, true, false>(sc, fp, block, d_out, d_counts, d_work, stream)
-                    : launch_t<TRAV_FAST, false, false>(sc, fp, block, d_out, d_counts, d_work, stream);
+    return d_counts ? launch_fast<true>(sc, fp, block, d_out, d_counts, d_work, stream)
+                    : launch_fast<false>(sc, fp, block, d_out, d_counts, d_work, stream);
 }
 
 hipError_t launch_gamma(const float* d_in, float* d_out, int64_t n, hipStream_t stream) {

@@ -50,13 +50,18 @@ def run(names):
         env["ENSEM3A_RT_LIB"] = os.path.join(VDIR, f"lib{name}.so")
         r = subprocess.run([sys.executable, "-c", CHECK], env=env, capture_output=True, text=True, timeout=300)
         parity = r.stdout.strip().splitlines()[-1] if r.returncode == 0 else "ERR " + r.stderr[-300:]
-        b = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "10", "--warmup", "2",
-                            "--no-cpu-baseline", "--bvh", os.environ.get("BVH", "sah")], env=env, capture_output=True, text=True, timeout=300)
-        try:
-            d = json.loads(b.stdout.strip().splitlines()[-1])
-            perf = f'{d["value"]:.1f} Msamples/s kernel {d["roofline"]["kernel_ms"]:.3f} ms'
-        except Exception:
-            perf = "ERR " + b.stderr[-300:]
+        perf = []
+        for cfg in os.environ.get("VAR_CONFIGS", "C2").split(","):
+            steps = "10" if cfg == "C2" else "2"
+            b = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--steps", steps, "--warmup", "1",
+                                "--no-cpu-baseline", "--config", cfg, "--bvh", os.environ.get("BVH", "sah")],
+                               env=env, capture_output=True, text=True, timeout=600)
+            try:
+                d = json.loads(b.stdout.strip().splitlines()[-1])
+                perf.append(f'{cfg} {d["value"]:.1f} Msamples/s ({d["roofline"]["kernel_ms"]:.2f} ms)')
+            except Exception:
+                perf.append(f"{cfg} ERR " + b.stderr[-300:])
+        perf = "; ".join(perf)
         print(f"{name}: {perf} | identical-vs-oracle {parity}", flush=True)
 
 
