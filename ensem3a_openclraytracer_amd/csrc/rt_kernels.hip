@@ -365,12 +365,114 @@ __device__ Hit trace_brute(const DevScene& S, rtm_f3 o, rtm_f3 d, Cnt& c) {
     return best;
 }
 
+// Brute force with ray-triangle pair compaction.  The lock-step loop above runs
+// the Moller-Trumbore block for the whole wave whenever any lane's box passes:
+// on C2 that is 28 of 36 triangles per ray round, at ~6 passing lanes each.
+// Here the box tests stay lock-step (scalar records), but every passing
+// (lane, triangle) pair is appended to a per-wave LDS queue; whenever the queue
+// holds a full wave of pairs, each lane takes one pair -- the owner's ray from
+// an LDS table, the triangle record by a vector load -- runs the same MT test
+// and folds the hit into the owner's best with one 64-bit LDS atomic min on
+// (distance bits, DFS position): positive float bits order like the floats, so
+// the minimum key is the reference's hit (lowest rank on equal distances).
+// Culling uses the owner's best as of the last batch (a conservative bound).
+constexpr int BRUTE_WAVE_LDS = 64 * 6 * 4 + 64 * 8 + 128 * 2;   // ray table | best keys | pair ring
+
+// Lanes of one wave hand data to each other through LDS here.  The hardware runs a
+// wave's LDS instructions in order; this keeps the compiler from reordering them
+// across the hand-off (it would otherwise move a lane's read of another lane's
+// entry above the write it depends on).
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+}
+
+template <bool COUNT>
+__device__ Hit trace_brute_compact(const DevScene& S, rtm_f3 o, rtm_f3 d, char* wl, Cnt& c) {
+    if (COUNT) c.rays++;
+    const unsigned lane = threadIdx.x & 63;
+    const unsigned long long act = __ballot(1);
+    const int nact = __popcll(act);
+    const int myrank = __popcll(act & ((1ull << lane) - 1ull));
+    float* ray = reinterpret_cast<float*>(wl);                                   // [6][64]
+    unsigned long long* bestk = reinterpret_cast<unsigned long long*>(wl + 64 * 6 * 4);
+    unsigned short* ring = reinterpret_cast<unsigned short*>(wl + 64 * 6 * 4 + 64 * 8);
+    ray[0 * 64 + lane] = o.x; ray[1 * 64 + lane] = o.y; ray[2 * 64 + lane] = o.z;
+    ray[3 * 64 + lane] = d.x; ray[4 * 64 + lane] = d.y; ray[5 * 64 + lane] = d.z;
+    const unsigned long long nokey = ((unsigned long long)__float_as_uint(1000.0f) << 32) | 0xffffffffull;
+    bestk[lane] = nokey;
+    wave_lds_sync();
+    const float ix = 1.0f / d.x, iy = 1.0f / d.y, iz = 1.0f / d.z;
+    const float oix = o.x * ix, oiy = o.y * iy, oiz = o.z * iz;
+    float bk = 1000.0f;
+    unsigned head = 0, tail = 0;   // wave-uniform ring positions
+    auto run_batch = [&](int n) __attribute__((always_inline)) {
+        if (myrank < n) {
+            const unsigned e = ring[(head + myrank) & 127];
+            const unsigned ow = e >> 8, q = e & 255;
+            const rtm_f3 ro = rtm_v3(ray[ow], ray[64 + ow], ray[128 + ow]);
+            const rtm_f3 rd = rtm_v3(ray[192 + ow], ray[256 + ow], ray[320 + ow]);
+            const float4 r1 = S.brute[4 * q + 1], r2 = S.brute[4 * q + 2], r3 = S.brute[4 * q + 3];
+            const rtm_f3 a = rtm_v3(r1.z, r1.w, r2.x), e1 = rtm_v3(r2.y, r2.z, r2.w), e2 = rtm_v3(r3.x, r3.y, r3.z);
+            const rtm_f3 h = rtm_cross(rd, e2);
+            const float det = rtm_dot(e1, h);
+            const float f = 1.0f / det;
+            const rtm_f3 sv = rtm_sub(ro, a);
+            const float u = f * rtm_dot(sv, h);
+            const rtm_f3 qv = rtm_cross(sv, e1);
+            const float v = f * rtm_dot(rd, qv);
+            const float k = f * rtm_dot(e2, qv);
+            const bool parallel = det > -0.0000001f && det < 0.0000001f;
+            const bool hit = !parallel && !(u < 0.0f || u > 1.0f) && !(v < 0.0f || u + v > 1.0f) &&
+                             (k > 0.0000001f) && k > 0.0001f && k < 1000.0f;
+            if (hit) atomicMin(&bestk[ow], ((unsigned long long)__float_as_uint(k) << 32) | q);
+        }
+        head += n;
+        wave_lds_sync();
+    };
+    for (int q = 0; q < S.nbrute; ++q) {
+        if (COUNT) count_wave(c.wave_trav);
+        const float4 r0 = sgpr4(S.brute[4 * q + 0]), r1 = sgpr4(S.brute[4 * q + 1]);
+        float tn, tx;
+        slab_fma(r0.x, r0.w, r0.y, r1.x, r0.z, r1.y, o.x, o.y, o.z, ix, iy, iz, oix, oiy, oiz, tn, tx);
+        const bool pass = fmaxf(tn, 0.0f) <= fminf(tx, bk * CULL_MARGIN);
+        if (COUNT) c.nodes++;
+        const unsigned long long m = __ballot(pass);
+        if (m == 0) continue;
+        if (COUNT && pass) c.tris++;
+        if (pass) ring[(tail + __popcll(m & ((1ull << lane) - 1ull))) & 127] = (unsigned short)((lane << 8) | q);
+        tail += __popcll(m);
+        wave_lds_sync();
+        if ((int)(tail - head) >= nact) {
+            run_batch(nact);
+            bk = __uint_as_float((unsigned)(bestk[lane] >> 32));
+        }
+    }
+    while (tail != head) run_batch(min((int)(tail - head), nact));
+    const unsigned long long key = bestk[lane];
+    Hit best{1000.0f, -1};
+    if (key != nokey) {
+        best.k = __uint_as_float((unsigned)(key >> 32));
+        best.tri = __float_as_int(S.brute[4 * (unsigned)(key & 0xffffffffu) + 3].w);
+    }
+    return best;
+}
+
+#ifndef RT_BRUTE_COMPACT
+#define RT_BRUTE_COMPACT 1
+#endif
+
 // stk/B: the REF traversal's int stack in LDS; st: the FAST traversal's stack.
 template <int TRAV, bool COUNT, bool SOA = false, bool OVF = false>
 __device__ __forceinline__ Hit trace(const DevScene& S, const float4* nodes, const float4* tris, rtm_f3 o, rtm_f3 d,
                                      int* stk, int B, const LaneStack& st, Cnt& c) {
     if (TRAV == TRAV_REF) return trace_ref<COUNT>(S, o, d, stk, B, c);
-    if (S.nbrute > 0) return trace_brute<COUNT>(S, o, d, c);
+    if (S.nbrute > 0) {
+        if (RT_BRUTE_COMPACT)
+            return trace_brute_compact<COUNT>(S, o, d, reinterpret_cast<char*>(stk - threadIdx.x) +
+                                                            (threadIdx.x >> 6) * BRUTE_WAVE_LDS, c);
+        return trace_brute<COUNT>(S, o, d, c);
+    }
     return trace_fast<COUNT, SOA, OVF>(S, nodes, tris, o, d, st, c);
 }
 
@@ -1157,6 +1259,8 @@ hipError_t launch_t(const DevScene& sc, const FrameParams& fp, int block, float*
     // FAST: int2 entries; the brute-force path of small scenes needs no stack
     const int depth = (TRAV == TRAV_REF) ? REF_STACK : (sc.nbrute > 0 ? 1 : 2 * (sc.stack_lds > 0 ? sc.stack_lds : 1));
     size_t lds = (size_t)depth * block * sizeof(int);
+    if (TRAV == TRAV_FAST && sc.nbrute > 0 && RT_BRUTE_COMPACT)
+        lds = std::max(lds, (size_t)(block / 64) * BRUTE_WAVE_LDS);
     if (SMEM) lds += (size_t)(4 * sc.nnodes + 3 * sc.ntri) * sizeof(float4);
     const int64_t need = (fp.nloc + block - 1) / block;
     if (need <= 0) return hipSuccess;
@@ -1251,7 +1355,9 @@ hipError_t launch_debug_trace(const DevScene& sc, int traversal, const float* ra
     s2.stack_lds = sc.depth > 0 ? sc.depth : 1;
     s2.stack_ovf = nullptr;
     const int depth = traversal == TRAV_REF ? REF_STACK : 2 * s2.stack_lds;
-    const size_t lds = (size_t)depth * block * sizeof(int);
+    size_t lds = (size_t)depth * block * sizeof(int);
+    if (traversal != TRAV_REF && sc.nbrute > 0 && RT_BRUTE_COMPACT)
+        lds = std::max(lds, (size_t)(block / 64) * BRUTE_WAVE_LDS);
     if (traversal == TRAV_REF)
         hipLaunchKernelGGL(debug_trace_kernel<TRAV_REF>, dim3((unsigned)((n + block - 1) / block)), dim3(block), lds,
                            stream, s2, rays, out, n);
