@@ -141,44 +141,87 @@ inline bool fidx(float v, int64_t limit, int32_t* out) {
 }
 
 // Emit the FAST node array from a binary tree with one triangle per leaf:
-// internal nodes in BFS order, each holding both child boxes and refs.
+// internal nodes in BFS order, each holding its children's boxes and refs.
 // box: 6 floats per tree node (lo.xyz, hi.xyz).
-void emit_bvh2(HostScene& hs, const int32_t* L, const int32_t* R, const int32_t* T, const float* box, int64_t nn) {
+//   RT_BVH_WIDTH 2: a node = its two children (rt_internal.h DevScene::nodes).
+//   RT_BVH_WIDTH 4: the binary tree is collapsed (an internal child with the largest
+//   surface area is replaced by its two children while fewer than 4), a node =
+//   8 float4: lo.x[4] hi.x[4] lo.y[4] hi.y[4] lo.z[4] hi.z[4] refs[4] unused; empty
+//   slots get a +inf box, which no slab test accepts.  Leaf boxes stay the reference's.
+void emit_bvh(HostScene& hs, const int32_t* L, const int32_t* R, const int32_t* T, const float* box, int64_t nn) {
+    constexpr int W = RT_BVH_WIDTH;
     auto is_inner = [&](int64_t i) { return L[i] >= 0; };
-    std::vector<int32_t> wide_of(nn, -1), depth_of(nn, 0), bfs;
-    bfs.reserve(nn);
-    int32_t max_depth = 1;
+    auto area = [&](int64_t i) {
+        const float* b = box + 6 * i;
+        const double x = (double)b[3] - b[0], y = (double)b[4] - b[1], z = (double)b[5] - b[2];
+        return x * y + y * z + z * x;
+    };
+    auto kids = [&](int32_t n) {
+        std::vector<int32_t> k{L[n], R[n]};
+        while ((int)k.size() < W) {
+            int best = -1;
+            for (int i = 0; i < (int)k.size(); ++i)
+                if (is_inner(k[i]) && (best < 0 || area(k[i]) > area(k[best]))) best = i;
+            if (best < 0) break;
+            const int32_t c = k[best];
+            k[best] = L[c];
+            k.insert(k.begin() + best + 1, R[c]);
+        }
+        return k;
+    };
+    std::vector<int32_t> wide_of(nn, -1), bfs;
+    std::vector<std::vector<int32_t>> children;
     if (is_inner(0)) {
         bfs.push_back(0);
         wide_of[0] = 0;
     }
     for (size_t h = 0; h < bfs.size(); ++h) {
-        const int32_t n = bfs[h];
-        for (int32_t ch : {L[n], R[n]}) {
+        children.push_back(kids(bfs[h]));
+        for (int32_t ch : children.back()) {
             if (!is_inner(ch)) continue;
             wide_of[ch] = (int32_t)bfs.size();
-            depth_of[ch] = depth_of[n] + 1;
-            max_depth = std::max(max_depth, depth_of[ch] + 1);
             bfs.push_back(ch);
         }
     }
+    // stack bound: a node pushes (children - 1) entries at most; need = max over root-to-leaf
+    // paths of the sum (children are after their parents in BFS order: sweep backwards)
+    std::vector<int32_t> need(bfs.size(), 0);
+    for (size_t w = bfs.size(); w-- > 0;) {
+        int32_t sub = 0;
+        for (int32_t ch : children[w])
+            if (is_inner(ch)) sub = std::max(sub, need[wide_of[ch]]);
+        need[w] = (int32_t)children[w].size() - 1 + sub;
+    }
+    constexpr int F = 4 * (W == 4 ? 8 : 4);   // floats per node
     hs.nnodes = (int32_t)bfs.size();
-    hs.nodes.assign((size_t)hs.nnodes * 16, 0.0f);
+    hs.nodes.assign((size_t)hs.nnodes * F, 0.0f);
     for (size_t w = 0; w < bfs.size(); ++w) {
-        const int32_t n = bfs[w];
-        const float* c0 = box + 6 * (int64_t)L[n];
-        const float* c1 = box + 6 * (int64_t)R[n];
-        float* o = hs.nodes.data() + 16 * w;
-        o[0] = c0[0]; o[1] = c0[3]; o[2] = c0[1]; o[3] = c0[4];
-        o[4] = c1[0]; o[5] = c1[3]; o[6] = c1[1]; o[7] = c1[4];
-        o[8] = c0[2]; o[9] = c0[5]; o[10] = c1[2]; o[11] = c1[5];
-        const int32_t r0 = is_inner(L[n]) ? wide_of[L[n]] : ~(48 * T[L[n]]);
-        const int32_t r1 = is_inner(R[n]) ? wide_of[R[n]] : ~(48 * T[R[n]]);
-        o[12] = as_f32(r0); o[13] = as_f32(r1); o[14] = 0.0f; o[15] = 0.0f;
+        float* o = hs.nodes.data() + (size_t)F * w;
+        const auto& ch = children[w];
+        auto ref = [&](int32_t c) { return is_inner(c) ? wide_of[c] : ~(48 * T[c]); };
+        if (W == 2) {
+            const float* c0 = box + 6 * (int64_t)ch[0];
+            const float* c1 = box + 6 * (int64_t)ch[1];
+            o[0] = c0[0]; o[1] = c0[3]; o[2] = c0[1]; o[3] = c0[4];
+            o[4] = c1[0]; o[5] = c1[3]; o[6] = c1[1]; o[7] = c1[4];
+            o[8] = c0[2]; o[9] = c0[5]; o[10] = c1[2]; o[11] = c1[5];
+            o[12] = as_f32(ref(ch[0])); o[13] = as_f32(ref(ch[1])); o[14] = 0.0f; o[15] = 0.0f;
+        } else {
+            for (int i = 0; i < 4; ++i) {
+                const bool used = i < (int)ch.size();
+                const float* b = used ? box + 6 * (int64_t)ch[i] : nullptr;
+                for (int a = 0; a < 3; ++a) {
+                    o[8 * a + i] = used ? b[a] : INFINITY;          // lo
+                    o[8 * a + 4 + i] = used ? b[3 + a] : INFINITY;  // hi
+                }
+                o[24 + i] = as_f32(used ? ref(ch[i]) : INT32_MIN);
+                o[28 + i] = 0.0f;
+            }
+        }
     }
     hs.root_ref = is_inner(0) ? 0 : ~(48 * T[0]);
     for (int k = 0; k < 6; ++k) hs.root_box[k] = box[k];
-    hs.depth = max_depth;
+    hs.depth = bfs.empty() ? 1 : std::max(1, need[0]);
 }
 
 // Pack the FAST layout from the reference export.  Returns false (with
@@ -283,13 +326,13 @@ bool pack_fast(HostScene& hs, const float* bvh9, int64_t nn, int64_t ntri, int l
         }
         rt::SahTree st;
         rt::sah_build(lb.data(), ids.data(), (int64_t)leaves.size(), st);
-        emit_bvh2(hs, st.L.data(), st.R.data(), st.leaf.data(), st.box.data(), (int64_t)st.L.size());
+        emit_bvh(hs, st.L.data(), st.R.data(), st.leaf.data(), st.box.data(), (int64_t)st.L.size());
         return true;
     }
     std::vector<float> box(6 * nn);
     for (int64_t i = 0; i < nn; ++i)
         for (int k = 0; k < 6; ++k) box[6 * i + k] = bvh9[9 * i + 2 + k];
-    emit_bvh2(hs, L.data(), R.data(), T.data(), box.data(), nn);
+    emit_bvh(hs, L.data(), R.data(), T.data(), box.data(), nn);
     return true;
 }
 
@@ -305,7 +348,7 @@ void pack_checked(HostScene& hs, const float* bvh9, int64_t nb, int64_t ntri, in
         hs.fast_ok = false;
         why = "tree deeper than 64 levels";
     }
-    if (hs.nodes.empty()) hs.nodes.assign(16, 0.0f);
+    if (hs.nodes.empty()) hs.nodes.assign(4 * rt::kNodeF4, 0.0f);
     if (hs.brute.empty()) hs.brute.assign(16, 0.0f);
 }
 
@@ -717,8 +760,8 @@ int rt_work_bytes(rt_ctx* ctx, double out[4]) {
     // Algorithmic bytes per unit: 32 B per box test (24 B AABB + 8 B child/leaf
     // refs), 36 B per triangle test (v0, e1, e2), 40 B per hit record, 16 B per IBL lookup.
     if (!ctx || !out) return set_err(ctx, RT_ERR_ARG, "null argument");
-    out[0] = effective_traversal(ctx) == RT_TRAVERSAL_FAST ? 64.0   // one BVH2 node = both child boxes
-                                                            : 32.0;  // one reference node = one box
+    out[0] = effective_traversal(ctx) == RT_TRAVERSAL_FAST ? 32.0 * RT_BVH_WIDTH  // a FAST node tests all its boxes
+                                                            : 32.0;                // one reference node = one box
     out[1] = 36.0;
     out[2] = 40.0;
     out[3] = 16.0;

@@ -11,6 +11,11 @@ namespace rt {
 #define RT_STACK_LDS 20
 #endif
 constexpr int kStackLds = RT_STACK_LDS;
+// FAST tree layout: 2 (BVH2, 4 float4 per node) or 4 (collapsed BVH4, 8 float4 per node)
+#ifndef RT_BVH_WIDTH
+#define RT_BVH_WIDTH 2
+#endif
+constexpr int kNodeF4 = RT_BVH_WIDTH == 4 ? 8 : 4;
 constexpr int kMaxLanesPerCu = 2048;   // resident threads per CU (gfx950)
 
 // Device view of one uploaded scene (all pointers are device pointers).

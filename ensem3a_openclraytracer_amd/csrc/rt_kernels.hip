@@ -226,6 +226,76 @@ __device__ __forceinline__ LaneStack lane_stack(const DevScene& S, int* lds_base
     return st;
 }
 
+// One FAST node: test every child box against the ray, push the hit children
+// except the nearest (farthest first, with their entry distance), and return the
+// nearest hit child, or INT_MIN when none is hit (pop next).  np: the node (AoS:
+// kNodeF4 consecutive float4; SOA: float4 planes kstride bytes apart).
+template <bool OVF>
+__device__ __forceinline__ int node_step(const char* np, unsigned kstride, rtm_f3 o, float ix, float iy, float iz,
+                                         float oix, float oiy, float oiz, float cull, const LaneStack& st,
+                                         unsigned& soff) {
+#if RT_BVH_WIDTH == 4
+    const float4 lx = *reinterpret_cast<const float4*>(np);
+    const float4 hx = *reinterpret_cast<const float4*>(np + kstride);
+    const float4 ly = *reinterpret_cast<const float4*>(np + 2 * kstride);
+    const float4 hy = *reinterpret_cast<const float4*>(np + 3 * kstride);
+    const float4 lz = *reinterpret_cast<const float4*>(np + 4 * kstride);
+    const float4 hz = *reinterpret_cast<const float4*>(np + 5 * kstride);
+    const int4 rf = *reinterpret_cast<const int4*>(np + 6 * kstride);
+    const float alx[4] = {lx.x, lx.y, lx.z, lx.w}, ahx[4] = {hx.x, hx.y, hx.z, hx.w};
+    const float aly[4] = {ly.x, ly.y, ly.z, ly.w}, ahy[4] = {hy.x, hy.y, hy.z, hy.w};
+    const float alz[4] = {lz.x, lz.y, lz.z, lz.w}, ahz[4] = {hz.x, hz.y, hz.z, hz.w};
+    float t[4];
+    int r[4] = {rf.x, rf.y, rf.z, rf.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        float tn, tx;
+        slab_fma(alx[i], ahx[i], aly[i], ahy[i], alz[i], ahz[i], o.x, o.y, o.z, ix, iy, iz, oix, oiy, oiz, tn, tx);
+        t[i] = fmaxf(tn, 0.0f) <= fminf(tx, cull) ? tn : INFINITY;   // misses sort last
+    }
+    auto ce = [&](int a, int b) __attribute__((always_inline)) {
+        const bool sw = t[b] < t[a];
+        const float ta = t[a], tb = t[b];
+        const int ra = r[a], rb = r[b];
+        t[a] = sw ? tb : ta; t[b] = sw ? ta : tb;
+        r[a] = sw ? rb : ra; r[b] = sw ? ra : rb;
+    };
+    ce(0, 1); ce(2, 3); ce(0, 2); ce(1, 3); ce(1, 2);
+#pragma unroll
+    for (int i = 3; i >= 1; --i) {
+        if (t[i] < INFINITY) {
+            st.template put<OVF>(soff, make_int2(r[i], __float_as_int(t[i])));
+            soff += st.stride;
+        }
+    }
+    return t[0] < INFINITY ? r[0] : INT_MIN;
+#else
+    const float4 a = *reinterpret_cast<const float4*>(np);
+    const float4 b = *reinterpret_cast<const float4*>(np + kstride);
+    const float4 z = *reinterpret_cast<const float4*>(np + 2 * kstride);
+    const int2 e = *reinterpret_cast<const int2*>(np + 3 * kstride);
+    float t0n, t0x, t1n, t1x;
+    slab_fma(a.x, a.y, a.z, a.w, z.x, z.y, o.x, o.y, o.z, ix, iy, iz, oix, oiy, oiz, t0n, t0x);
+    slab_fma(b.x, b.y, b.z, b.w, z.z, z.w, o.x, o.y, o.z, ix, iy, iz, oix, oiy, oiz, t1n, t1x);
+#if RT_HIT3
+    // t0x >= t0n && t0x >= 0 && t0n <= cull, for the never-NaN slab values and cull > 0
+    const bool h0 = fmaxf(t0n, 0.0f) <= fminf(t0x, cull);
+    const bool h1 = fmaxf(t1n, 0.0f) <= fminf(t1x, cull);
+#else
+    const bool h0 = t0x >= t0n && t0x >= 0.0f && t0n <= cull;
+    const bool h1 = t1x >= t1n && t1x >= 0.0f && t1n <= cull;
+#endif
+    if (h0 && h1) {
+        const bool first0 = t0n <= t1n;
+        st.template put<OVF>(soff, make_int2(first0 ? e.y : e.x, __float_as_int(first0 ? t1n : t0n)));
+        soff += st.stride;
+        return first0 ? e.x : e.y;
+    }
+    if (h0 || h1) return h0 ? e.x : e.y;
+    return INT_MIN;
+#endif
+}
+
 // One item per iteration: an internal node (both child boxes tested, nearer hit
 // child continues, the farther is pushed with its entry distance) or a leaf
 // (one triangle test).  Popped items whose entry distance is beyond the best hit
@@ -258,32 +328,10 @@ __device__ Hit trace_fast(const DevScene& S, const float4* __restrict__ nodes, c
         if (COUNT) count_wave(c.wave_trav);
         if (item >= 0) {
             if (COUNT) c.nodes++;
-            const char* np = nb + (SOA ? 16u : 64u) * (unsigned)item;
-            const float4 a = *reinterpret_cast<const float4*>(np);
-            const float4 b = *reinterpret_cast<const float4*>(np + kstride);
-            const float4 z = *reinterpret_cast<const float4*>(np + 2 * kstride);
-            const int2 e = *reinterpret_cast<const int2*>(np + 3 * kstride);
-            float t0n, t0x, t1n, t1x;
-            slab_fma(a.x, a.y, a.z, a.w, z.x, z.y, o.x, o.y, o.z, ix, iy, iz, oix, oiy, oiz, t0n, t0x);
-            slab_fma(b.x, b.y, b.z, b.w, z.z, z.w, o.x, o.y, o.z, ix, iy, iz, oix, oiy, oiz, t1n, t1x);
-            const float cull = best.k * CULL_MARGIN;
-#if RT_HIT3
-            // t0x >= t0n && t0x >= 0 && t0n <= cull, for the never-NaN slab values and cull > 0
-            const bool h0 = fmaxf(t0n, 0.0f) <= fminf(t0x, cull);
-            const bool h1 = fmaxf(t1n, 0.0f) <= fminf(t1x, cull);
-#else
-            const bool h0 = t0x >= t0n && t0x >= 0.0f && t0n <= cull;
-            const bool h1 = t1x >= t1n && t1x >= 0.0f && t1n <= cull;
-#endif
-            if (h0 && h1) {
-                const bool first0 = t0n <= t1n;
-                st.template put<OVF>(soff, make_int2(first0 ? e.y : e.x, __float_as_int(first0 ? t1n : t0n)));
-                soff += sstride;
-                item = first0 ? e.x : e.y;
-                continue;
-            }
-            if (h0 || h1) {
-                item = h0 ? e.x : e.y;
+            const char* np = nb + (SOA ? 16u : 16u * kNodeF4) * (unsigned)item;
+            const int next = node_step<OVF>(np, kstride, o, ix, iy, iz, oix, oiy, oiz, best.k * CULL_MARGIN, st, soff);
+            if (next != INT_MIN) {
+                item = next;
                 continue;
             }
         } else {
@@ -723,8 +771,9 @@ __global__ void RT_RENDER_BOUNDS render_kernel(DevScene S, FrameParams F, float*
     const float4* tris = S.tri_geo;
     if (SMEM) {
         float4* ln = reinterpret_cast<float4*>(lds_stack + 2 * S.stack_lds * B);
-        float4* lt = ln + 4 * S.nnodes;
-        for (int q = threadIdx.x; q < 4 * S.nnodes; q += B) ln[(q & 3) * S.nnodes + (q >> 2)] = S.nodes[q];
+        float4* lt = ln + kNodeF4 * S.nnodes;
+        for (int q = threadIdx.x; q < kNodeF4 * S.nnodes; q += B)
+            ln[(q % kNodeF4) * S.nnodes + q / kNodeF4] = S.nodes[q];
         for (int q = threadIdx.x; q < 3 * S.ntri; q += B) lt[q] = S.tri_geo[q];
         __syncthreads();
         nodes = ln;
@@ -970,27 +1019,8 @@ __device__ __forceinline__ bool fast_round(const DevScene& S, FastRay& R, const 
     const float oix = R.o.x * R.ix, oiy = R.o.y * R.iy, oiz = R.o.z * R.iz;
     while (R.item >= 0) {
         if (COUNT) { count_wave(c.wave_trav); c.nodes++; }
-        const char* np = nb + (SOA ? 16u : 64u) * (unsigned)R.item;
-        const float4 a = *reinterpret_cast<const float4*>(np);
-        const float4 b = *reinterpret_cast<const float4*>(np + kstride);
-        const float4 z = *reinterpret_cast<const float4*>(np + 2 * kstride);
-        const int2 e = *reinterpret_cast<const int2*>(np + 3 * kstride);
-        float t0n, t0x, t1n, t1x;
-        slab_fma(a.x, a.y, a.z, a.w, z.x, z.y, R.o.x, R.o.y, R.o.z, R.ix, R.iy, R.iz, oix, oiy, oiz, t0n, t0x);
-        slab_fma(b.x, b.y, b.z, b.w, z.z, z.w, R.o.x, R.o.y, R.o.z, R.ix, R.iy, R.iz, oix, oiy, oiz, t1n, t1x);
-        const float cull = R.bk * CULL_MARGIN;
-        const bool h0 = fmaxf(t0n, 0.0f) <= fminf(t0x, cull);
-        const bool h1 = fmaxf(t1n, 0.0f) <= fminf(t1x, cull);
-        if (h0 && h1) {
-            const bool first0 = t0n <= t1n;
-            st.template put<OVF>(R.soff, make_int2(first0 ? e.y : e.x, __float_as_int(first0 ? t1n : t0n)));
-            R.soff += sstride;
-            R.item = first0 ? e.x : e.y;
-        } else if (h0 || h1) {
-            R.item = h0 ? e.x : e.y;
-        } else {
-            R.item = INT_MIN;      // nothing hit below this node: pop (never a leaf ref: those are ~(48 t))
-        }
+        const char* np = nb + (SOA ? 16u : 16u * kNodeF4) * (unsigned)R.item;
+        R.item = node_step<OVF>(np, kstride, R.o, R.ix, R.iy, R.iz, oix, oiy, oiz, R.bk * CULL_MARGIN, st, R.soff);
     }
     if (R.item != INT_MIN) {      // a leaf: one triangle test
         if (COUNT) { count_wave(c.wave_trav); c.tris++; }
@@ -1037,8 +1067,9 @@ __global__ void RT_RESUME_BOUNDS render_resume_kernel(DevScene S, FrameParams F,
     const float4* tris = S.tri_geo;
     if (SMEM) {
         float4* ln = reinterpret_cast<float4*>(lds_stack + 2 * S.stack_lds * B);
-        float4* lt = ln + 4 * S.nnodes;
-        for (int q = threadIdx.x; q < 4 * S.nnodes; q += B) ln[(q & 3) * S.nnodes + (q >> 2)] = S.nodes[q];
+        float4* lt = ln + kNodeF4 * S.nnodes;
+        for (int q = threadIdx.x; q < kNodeF4 * S.nnodes; q += B)
+            ln[(q % kNodeF4) * S.nnodes + q / kNodeF4] = S.nodes[q];
         for (int q = threadIdx.x; q < 3 * S.ntri; q += B) lt[q] = S.tri_geo[q];
         __syncthreads();
         nodes = ln;
@@ -1261,7 +1292,7 @@ hipError_t launch_t(const DevScene& sc, const FrameParams& fp, int block, float*
     size_t lds = (size_t)depth * block * sizeof(int);
     if (TRAV == TRAV_FAST && sc.nbrute > 0 && RT_BRUTE_COMPACT)
         lds = std::max(lds, (size_t)(block / 64) * BRUTE_WAVE_LDS);
-    if (SMEM) lds += (size_t)(4 * sc.nnodes + 3 * sc.ntri) * sizeof(float4);
+    if (SMEM) lds += (size_t)(kNodeF4 * sc.nnodes + 3 * sc.ntri) * sizeof(float4);
     const int64_t need = (fp.nloc + block - 1) / block;
     if (need <= 0) return hipSuccess;
     // persistent grid: as many blocks as the device keeps resident (pixels are handed out by d_work)
@@ -1370,7 +1401,7 @@ hipError_t launch_debug_trace(const DevScene& sc, int traversal, const float* ra
 template <bool COUNT>
 hipError_t launch_fast(const DevScene& sc, const FrameParams& fp, int block, float* d_out,
                        unsigned long long* d_counts, unsigned int* d_work, hipStream_t stream) {
-    const size_t scene_bytes = (size_t)(4 * sc.nnodes + 3 * sc.ntri) * sizeof(float4);
+    const size_t scene_bytes = (size_t)(kNodeF4 * sc.nnodes + 3 * sc.ntri) * sizeof(float4);
     const bool smem = sc.ntri > 0 && sc.nbrute == 0 && scene_bytes <= (size_t)RT_LDS_SCENE_MAX;
     const bool ovf = sc.nbrute == 0 && sc.stack_lds < sc.depth;
     const bool resume = sc.ntri > 0 && sc.nbrute == 0 && fp.resume_min > 0;
