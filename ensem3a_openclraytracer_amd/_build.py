@@ -18,7 +18,7 @@ LIBDIR = os.path.join(PKG, "lib")
 LIB = os.path.join(LIBDIR, "libensem3a_rt.so")
 OBJDIR = os.path.join(ROOT, "build", "native")
 
-SOURCES = ["rt_kernels.hip", "rt_api.hip", "bvh_build.cpp", "bvh_sah.cpp"]
+SOURCES = ["rt_kernels.hip", "rt_api.hip", "bvh_build.cpp", "bvh_sah.cpp", "obj_load.cpp"]
 HEADERS = ["rt_internal.h", "rtm.h", "bvh_sah.h"]
 # -ffp-contract=off: the numerics contract (rtm.h) places every fused multiply-add explicitly.
 COMMON = ["-O3", "-std=c++17", "-ffp-contract=off", "-fno-fast-math", "-fno-slp-vectorize", "-fPIC", "-Wall",
@@ -47,7 +47,7 @@ def build(verbose: bool = False, force: bool = False, defines=(), out: str = Non
     os.makedirs(objdir, exist_ok=True)
     os.makedirs(os.path.dirname(lib_path), exist_ok=True)
     hdrs = [os.path.join(CSRC, h) for h in HEADERS] + [os.path.join(ROOT, "include", h)
-                                                      for h in ("rt_api.h", "rt_debug.h")]
+                                                      for h in ("rt_api.h", "rt_debug.h", "rt_scene.h")]
     jobs = []
     objs = []
     for src in SOURCES:

@@ -27,6 +27,7 @@ EXPORTED = (
     "rt_render", "rt_render_device", "rt_tile_rows", "rt_count_work", "rt_work_bytes", "rt_gamma",
     "rt_bvh_build", "rt_device_count", "rt_debug_math", "rt_debug_trace", "rt_debug_scene_info", "rt_debug_pixel_log",
     "rt_debug_wave_counts",
+    "rt_obj_parse", "rt_obj_size", "rt_obj_copy", "rt_obj_free", "rt_obj_last_error",
 )
 
 _c_p = ctypes.c_void_p
@@ -78,6 +79,11 @@ def lib():
             "rt_gamma": (_i32, [_c_p, _c_p, _c_p, _i64]),
             "rt_bvh_build": (_i32, [_c_p, _i64, _c_p, _i64, _c_p, ctypes.POINTER(_i64)]),
             "rt_device_count": (_i32, []),
+            "rt_obj_parse": (_i32, [_c_p, _i64, ctypes.POINTER(_c_p)]),
+            "rt_obj_size": (_i64, [_c_p, _i32]),
+            "rt_obj_copy": (_i32, [_c_p, _c_p, _c_p, _c_p, _c_p]),
+            "rt_obj_free": (None, [_c_p]),
+            "rt_obj_last_error": (ctypes.c_char_p, []),
             "rt_debug_math": (_i32, [_c_p, _i32, _c_p, _c_p, _c_p, _i64]),
             "rt_debug_trace": (_i32, [_c_p, _i32, _c_p, _c_p, _i64]),
             "rt_debug_scene_info": (_i32, [_c_p, _c_p]),
@@ -237,6 +243,23 @@ class Context:
         out = np.zeros(4, dtype=np.int64)
         self._check(lib().rt_debug_scene_info(self.handle, out.ctypes.data))
         return dict(fast_ok=bool(out[0]), depth=int(out[1]), nodes=int(out[2]), tris=int(out[3]))
+
+
+def parse_obj(text):
+    """Native OBJ import (include/rt_scene.h): ``(V_p, V_n, V_uv, faceData, matCounter)``
+    with the reference importer's semantics (FileManager.py:253-304).  Host only."""
+    data = text.encode() if isinstance(text, str) else bytes(text)
+    h = _c_p()
+    if lib().rt_obj_parse(data, len(data), ctypes.byref(h)) != 0:
+        raise ValueError("OBJ parse failed: " + lib().rt_obj_last_error().decode(errors="replace"))
+    try:
+        n = [int(lib().rt_obj_size(h, k)) for k in range(5)]
+        vp, vn, vuv = (np.zeros(n[k], np.float32) for k in range(3))
+        face = np.zeros(n[3], np.int32)
+        lib().rt_obj_copy(h, vp.ctypes.data, vn.ctypes.data, vuv.ctypes.data, face.ctypes.data)
+    finally:
+        lib().rt_obj_free(h)
+    return vp, vn, vuv, face, n[4]
 
 
 def tile_rows(npix: int, width: int, row0: int, row_step: int) -> int:

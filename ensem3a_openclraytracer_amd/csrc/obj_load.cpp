@@ -1,0 +1,203 @@
+// Native OBJ import with the reference importer's semantics (include/rt_scene.h).
+//
+// Reproduces FileManager.Scene's parse (FileManager.py:253-304) byte for byte:
+//   * v / vn / vt lines anywhere in the file fill V_p / V_n / V_uv in file order
+//     (the reference reads them through pywavefront: whitespace-separated
+//     fields, decimal text -> double -> float32);
+//   * lines before the first line whose first space-separated field is exactly
+//     "usemtl" are otherwise ignored (faces there are lost);
+//   * after it, a line starting with 'f' is one triangle "f p/uv/n p/uv/n p/uv/n"
+//     (fields split on single spaces, only the first three vertices, 1-based
+//     indices made 0-based), stored [mat, uv0..2, n0..2, p0..2]
+//     (FileManager.py:276-282);
+//   * any other line starting with 'u' increments the material counter.
+// A face field the reference's int() would reject makes the parse fail.
+#include <cerrno>
+#include <cmath>
+#include <cstdint>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/rt_scene.h"
+
+struct rt_obj {
+    std::vector<float> vp, vn, vuv;
+    std::vector<int32_t> face;
+    int64_t mat_counter = 0;
+};
+
+namespace {
+
+thread_local std::string g_obj_error;
+
+int fail(const std::string& msg) {
+    g_obj_error = msg;
+    return 1;
+}
+
+bool is_space(char c) { return c == ' ' || c == '\t' || c == '\n' || c == '\r' || c == '\f' || c == '\v'; }
+
+// Python float(): the whole field must be a number (surrounding whitespace is already split off).
+bool parse_float(const char* b, const char* e, double* out) {
+    std::string s(b, e);
+    if (s.empty()) return false;
+    char* end = nullptr;
+    errno = 0;
+    const double v = std::strtod(s.c_str(), &end);
+    if (end != s.c_str() + s.size()) return false;
+    *out = v;   // overflow gives +-inf like Python's float() does for huge literals
+    return true;
+}
+
+// Python int() on a field: optional surrounding whitespace, optional sign, decimal digits.
+bool parse_int(const char* b, const char* e, long long* out) {
+    while (b < e && is_space(*b)) ++b;
+    while (e > b && is_space(e[-1])) --e;
+    if (b == e) return false;
+    const char* p = b;
+    if (*p == '+' || *p == '-') ++p;
+    if (p == e) return false;
+    for (const char* q = p; q < e; ++q)
+        if (*q < '0' || *q > '9') return false;
+    *out = std::strtoll(std::string(b, e).c_str(), nullptr, 10);
+    return true;
+}
+
+// Whitespace-separated fields of [b, e).
+void split_ws(const char* b, const char* e, std::vector<std::pair<const char*, const char*>>& f) {
+    f.clear();
+    const char* p = b;
+    while (p < e) {
+        while (p < e && is_space(*p)) ++p;
+        if (p == e) break;
+        const char* s = p;
+        while (p < e && !is_space(*p)) ++p;
+        f.emplace_back(s, p);
+    }
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* rt_obj_last_error(void) { return g_obj_error.c_str(); }
+
+int rt_obj_parse(const char* text, int64_t len, rt_obj** out) {
+    if (!out || (!text && len > 0) || len < 0) return fail("bad arguments");
+    *out = nullptr;
+    rt_obj* o = new rt_obj();
+    std::vector<std::pair<const char*, const char*>> ws;
+    bool seen_usemtl = false;
+    const char* p = text;
+    const char* end = text + len;
+    int64_t lineno = 0;
+    while (p < end) {
+        const char* nl = static_cast<const char*>(std::memchr(p, '\n', (size_t)(end - p)));
+        const char* le = nl ? nl + 1 : end;   // the line including its '\n', as Python iterates it
+        ++lineno;
+        split_ws(p, le, ws);
+        if (!ws.empty()) {
+            const std::string head(ws[0].first, ws[0].second);
+            if (head == "v" || head == "vn") {
+                if (ws.size() < 4) { delete o; return fail("line " + std::to_string(lineno) + ": short vertex"); }
+                for (int k = 1; k <= 3; ++k) {
+                    double v;
+                    if (!parse_float(ws[k].first, ws[k].second, &v)) {
+                        delete o;
+                        return fail("line " + std::to_string(lineno) + ": bad number");
+                    }
+                    (head == "v" ? o->vp : o->vn).push_back((float)v);
+                }
+            } else if (head == "vt") {
+                double u = 0.0, v = 0.0;
+                if (ws.size() < 2 || !parse_float(ws[1].first, ws[1].second, &u) ||
+                    (ws.size() > 2 && !parse_float(ws[2].first, ws[2].second, &v))) {
+                    delete o;
+                    return fail("line " + std::to_string(lineno) + ": bad texture coordinate");
+                }
+                o->vuv.push_back((float)u);
+                o->vuv.push_back((float)v);
+            }
+        }
+        if (!seen_usemtl) {
+            // line.split(" ")[0] == "usemtl"
+            const char* sp = static_cast<const char*>(std::memchr(p, ' ', (size_t)(le - p)));
+            const char* fe = sp ? sp : le;
+            if (fe - p == 6 && std::memcmp(p, "usemtl", 6) == 0) seen_usemtl = true;
+            p = le;
+            continue;
+        }
+        if (*p == 'f') {
+            // parts = line.split(" "); parts[1..3] = "p/uv/n"
+            const char* fields[5];
+            const char* fends[5];
+            int nf = 0;
+            const char* q = p;
+            while (nf < 5) {
+                const char* sp = static_cast<const char*>(std::memchr(q, ' ', (size_t)(le - q)));
+                fields[nf] = q;
+                fends[nf] = sp ? sp : le;
+                ++nf;
+                if (!sp) break;
+                q = sp + 1;
+            }
+            if (nf < 4) { delete o; return fail("line " + std::to_string(lineno) + ": face with fewer than 3 vertices"); }
+            int32_t row[10];
+            row[0] = (int32_t)o->mat_counter;
+            const int comps[3] = {1, 2, 0};   // uv, normal, position
+            int w = 1;
+            for (int ci = 0; ci < 3; ++ci) {
+                for (int j = 1; j <= 3; ++j) {
+                    // field.split("/")[comp]
+                    const char* s = fields[j];
+                    const char* fe = fends[j];
+                    for (int skip = 0; skip < comps[ci]; ++skip) {
+                        const char* sl = static_cast<const char*>(std::memchr(s, '/', (size_t)(fe - s)));
+                        if (!sl) { delete o; return fail("line " + std::to_string(lineno) + ": face vertex without uv/normal"); }
+                        s = sl + 1;
+                    }
+                    const char* sl = static_cast<const char*>(std::memchr(s, '/', (size_t)(fe - s)));
+                    long long v;
+                    if (!parse_int(s, sl ? sl : fe, &v)) {
+                        delete o;
+                        return fail("line " + std::to_string(lineno) + ": bad face index");
+                    }
+                    row[w++] = (int32_t)(v - 1);
+                }
+            }
+            o->face.insert(o->face.end(), row, row + 10);
+        } else if (*p == 'u') {
+            ++o->mat_counter;
+        }
+        p = le;
+    }
+    *out = o;
+    return 0;
+}
+
+int64_t rt_obj_size(const rt_obj* o, int what) {
+    if (!o) return -1;
+    switch (what) {
+        case RT_OBJ_VP: return (int64_t)o->vp.size();
+        case RT_OBJ_VN: return (int64_t)o->vn.size();
+        case RT_OBJ_VUV: return (int64_t)o->vuv.size();
+        case RT_OBJ_FACE: return (int64_t)o->face.size();
+        case RT_OBJ_MATERIALS: return o->mat_counter;
+        default: return -1;
+    }
+}
+
+int rt_obj_copy(const rt_obj* o, float* vp, float* vn, float* vuv, int32_t* face) {
+    if (!o) return fail("null handle");
+    if (vp && !o->vp.empty()) std::memcpy(vp, o->vp.data(), o->vp.size() * sizeof(float));
+    if (vn && !o->vn.empty()) std::memcpy(vn, o->vn.data(), o->vn.size() * sizeof(float));
+    if (vuv && !o->vuv.empty()) std::memcpy(vuv, o->vuv.data(), o->vuv.size() * sizeof(float));
+    if (face && !o->face.empty()) std::memcpy(face, o->face.data(), o->face.size() * sizeof(int32_t));
+    return 0;
+}
+
+void rt_obj_free(rt_obj* o) { delete o; }
+
+}  // extern "C"

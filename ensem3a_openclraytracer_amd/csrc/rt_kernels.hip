@@ -596,6 +596,16 @@ __device__ rtm_f3 sample_ibl(const DevScene& S, const LaunchConst& C, rtm_f3 dir
     return rtm_scale(rtm_v3(sr * w, sg * w, sb * w), 1.0f);
 }
 
+// IBL radiance where it can matter: every texel mean is a finite value >= 0, so
+// with IBL_Power == 0 (C1/C2) the reference's IBL(dir) * IBL_Power is exactly
+// 0 * IBL_Power for any dir, and the lookup is skipped.
+template <bool COUNT>
+__device__ __forceinline__ rtm_f3 sample_ibl_if(const DevScene& S, const LaunchConst& C, rtm_f3 dir, float power,
+                                               Cnt& c) {
+    if (power == 0.0f) return rtm_v3(0.0f, 0.0f, 0.0f);
+    return sample_ibl<COUNT>(S, C, dir, c);
+}
+
 // ---- hemisphere samplers, MathLib.cl:313-366, with the triangle's frame
 // (colinear flag, rotation to the normal, normalize(n)) precomputed by
 // prep_frames_kernel: f0/f1 = q/qinv of the rotation, f2 = normalize(n) | colinear ----
@@ -843,7 +853,7 @@ __global__ void RT_RENDER_BOUNDS render_kernel(DevScene S, FrameParams F, float*
             if (j > maxB) {
                 // naiveGI's loop never entered (maxBounce < 0): the sample stays 1
             } else if (tri < 0) {
-                so = rtm_scale(rtm_mul(so, sample_ibl<COUNT>(S, C, Rd, c)), e4);
+                so = rtm_scale(rtm_mul(so, sample_ibl_if<COUNT>(S, C, Rd, e4, c)), e4);
             } else {
                 const float4 sh = S.tri_shade[tri];
                 const rtm_f3 n = xyz(sh);
@@ -942,7 +952,7 @@ __global__ void RT_RENDER_BOUNDS render_kernel(DevScene S, FrameParams F, float*
                 const Mat sm = load_mat(S.mat, __float_as_int(S.tri_shade[h.tri].w));
                 if (sm.type == 3) sunLight = rtm_scale(sm.color, e3);
             }
-            const rtm_f3 envLight = rtm_scale(sample_ibl<COUNT>(S, C, Bd, c), e4);
+            const rtm_f3 envLight = rtm_scale(sample_ibl_if<COUNT>(S, C, Bd, e4, c), e4);
             so = rtm_mul(so, rtm_add(sunLight, envLight));
             finish = true;
         }
@@ -1210,7 +1220,7 @@ __global__ void RT_RESUME_BOUNDS render_resume_kernel(DevScene S, FrameParams F,
                     const Mat sm = load_mat(S.mat, __float_as_int(S.tri_shade[h.tri].w));
                     if (sm.type == 3) sunLight = rtm_scale(sm.color, e3);
                 }
-                const rtm_f3 envLight = rtm_scale(sample_ibl<COUNT>(S, C, Bd, c), e4);
+                const rtm_f3 envLight = rtm_scale(sample_ibl_if<COUNT>(S, C, Bd, e4, c), e4);
                 so = rtm_mul(so, rtm_add(sunLight, envLight));
                 finish_sample();
             }
@@ -1219,7 +1229,7 @@ __global__ void RT_RESUME_BOUNDS render_resume_kernel(DevScene S, FrameParams F,
                 if (j > maxB) {
                     finish_sample();   // naiveGI's loop never entered (maxBounce < 0): the sample stays 1
                 } else if (tri < 0) {
-                    so = rtm_scale(rtm_mul(so, sample_ibl<COUNT>(S, C, Rd, c)), e4);
+                    so = rtm_scale(rtm_mul(so, sample_ibl_if<COUNT>(S, C, Rd, e4, c)), e4);
                     finish_sample();
                 } else {
                     const float4 sh = S.tri_shade[tri];

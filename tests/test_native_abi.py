@@ -15,7 +15,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 def _declared():
     names = set()
-    for h in ("rt_api.h", "rt_debug.h"):
+    for h in ("rt_api.h", "rt_debug.h", "rt_scene.h"):
         with open(os.path.join(ROOT, "include", h)) as f:
             txt = f.read()
         names |= set(re.findall(r"\b(rt_[a-z_]+)\s*\(", txt))

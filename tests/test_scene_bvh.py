@@ -114,3 +114,59 @@ def test_c3_overrides():
     m = sc.materialData.reshape(-1, 6)
     np.testing.assert_allclose(m[4, :4], [3, 0.88, 1, 1], rtol=1e-7)
     assert m[0, 0] == 2 and m[0, 4] == np.float32(0.2)
+
+
+# ---- native OBJ import (include/rt_scene.h) ----
+# The bundled OBJ files are read from the reference checkout when it is present (this
+# container); the CPU suite only.
+SCENE_DIR = "/root/reference/ObjFiles"
+
+def _same(a, b):
+    return a.dtype == b.dtype and a.shape == b.shape and np.array_equal(a.view(np.uint8), b.view(np.uint8))
+
+
+@pytest.mark.parametrize("name", ["Cornell box", "Cornell box_Monkey", "Serre_leger", "protoEnsem", "FurnaceHD"])
+def test_native_obj_parse_matches_python(name):
+    """The C++ importer returns the Python mirror's arrays bit for bit on every bundled scene."""
+    from ensem3a_openclraytracer_amd import _native
+    path = os.path.join(SCENE_DIR, name + ".obj")
+    if not os.path.exists(path):
+        pytest.skip("bundled OBJ text not available")
+    with open(path) as f:
+        text = f.read()
+    py = parse_obj(text)
+    nat = _native.parse_obj(text)
+    for a, b in zip(py[:4], nat[:4]):
+        assert _same(a, b)
+    assert py[4] == nat[4]
+
+
+def test_native_obj_parse_quirks():
+    from ensem3a_openclraytracer_amd import _native
+    text = ("# comment\nv 0 0 0\nv 1 0 0\nv 0 1 0\nvn 0 0 1\nvt 0.5\nvt 0.25 0.75\n"
+            "f 1/1/1 2/2/1 3/1/1\n"                      # before the first usemtl: lost
+            "usemtl a\nf 1/1/1 2/2/1 3/1/1\nu second\n"  # any 'u' line counts as a material
+            "usemtl b\nf 3/2/1 2/1/1 1/2/1 4/4/4\n"       # only three vertices are read
+            "usemtl\nf 1/2/1 2/2/1 3/2/1")                # no trailing newline
+    py = parse_obj(text)
+    nat = _native.parse_obj(text)
+    for a, b in zip(py[:4], nat[:4]):
+        assert _same(a, b)
+    assert py[4] == nat[4] == 3
+    assert nat[3].reshape(-1, 10)[:, 0].tolist() == [0, 2, 3]
+    with pytest.raises(ValueError):
+        _native.parse_obj("usemtl a\nf 1//1 2/2/2\n")       # two vertices
+    with pytest.raises(ValueError):
+        _native.parse_obj("usemtl a\nf 1 2 3\n")             # no uv / normal indices
+    with pytest.raises(ValueError):
+        _native.parse_obj("v 1 2\n")
+
+
+def test_native_obj_parse_grid1m_matches_python():
+    from ensem3a_openclraytracer_amd import _native
+    from ensem3a_openclraytracer_amd import workloads as W
+    text = W.grid_obj_text(60)
+    py = parse_obj(text)
+    nat = _native.parse_obj(text)
+    for a, b in zip(py[:4], nat[:4]):
+        assert _same(a, b)
