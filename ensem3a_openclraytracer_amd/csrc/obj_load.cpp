@@ -12,7 +12,7 @@
 //     (FileManager.py:276-282);
 //   * any other line starting with 'u' increments the material counter.
 // A face field the reference's int() would reject makes the parse fail.
-#include <cerrno>
+#include <charconv>
 #include <cmath>
 #include <cstdint>
 #include <cstdlib>
@@ -39,16 +39,18 @@ int fail(const std::string& msg) {
 
 bool is_space(char c) { return c == ' ' || c == '\t' || c == '\n' || c == '\r' || c == '\f' || c == '\v'; }
 
-// Python float(): the whole field must be a number (surrounding whitespace is already split off).
+// Python float(): the whole field must be a number (surrounding whitespace is already split off);
+// correctly rounded like Python's, via std::from_chars (which takes no leading '+').
 bool parse_float(const char* b, const char* e, double* out) {
-    std::string s(b, e);
-    if (s.empty()) return false;
-    char* end = nullptr;
-    errno = 0;
-    const double v = std::strtod(s.c_str(), &end);
-    if (end != s.c_str() + s.size()) return false;
-    *out = v;   // overflow gives +-inf like Python's float() does for huge literals
-    return true;
+    if (b == e) return false;
+    const char* p = (*b == '+' && e - b > 1 && b[1] != '-' && b[1] != '+') ? b + 1 : b;
+    const auto r = std::from_chars(p, e, *out, std::chars_format::general);
+    if (r.ec == std::errc::result_out_of_range) {   // Python: huge literals -> +-inf, tiny -> +-0
+        const std::string s(b, e);
+        *out = std::strtod(s.c_str(), nullptr);
+        return true;
+    }
+    return r.ec == std::errc() && r.ptr == e;
 }
 
 // Python int() on a field: optional surrounding whitespace, optional sign, decimal digits.
@@ -56,12 +58,15 @@ bool parse_int(const char* b, const char* e, long long* out) {
     while (b < e && is_space(*b)) ++b;
     while (e > b && is_space(e[-1])) --e;
     if (b == e) return false;
-    const char* p = b;
-    if (*p == '+' || *p == '-') ++p;
-    if (p == e) return false;
-    for (const char* q = p; q < e; ++q)
+    bool neg = false;
+    if (*b == '+' || *b == '-') neg = *b++ == '-';
+    if (b == e) return false;
+    long long v = 0;
+    for (const char* q = b; q < e; ++q) {
         if (*q < '0' || *q > '9') return false;
-    *out = std::strtoll(std::string(b, e).c_str(), nullptr, 10);
+        v = v * 10 + (*q - '0');
+    }
+    *out = neg ? -v : v;
     return true;
 }
 
@@ -99,8 +104,12 @@ int rt_obj_parse(const char* text, int64_t len, rt_obj** out) {
         ++lineno;
         split_ws(p, le, ws);
         if (!ws.empty()) {
-            const std::string head(ws[0].first, ws[0].second);
-            if (head == "v" || head == "vn") {
+            const size_t hl = (size_t)(ws[0].second - ws[0].first);
+            const char* hp = ws[0].first;
+            const bool is_v = hl == 1 && hp[0] == 'v';
+            const bool is_vn = hl == 2 && hp[0] == 'v' && hp[1] == 'n';
+            const bool is_vt = hl == 2 && hp[0] == 'v' && hp[1] == 't';
+            if (is_v || is_vn) {
                 if (ws.size() < 4) { delete o; return fail("line " + std::to_string(lineno) + ": short vertex"); }
                 for (int k = 1; k <= 3; ++k) {
                     double v;
@@ -108,9 +117,9 @@ int rt_obj_parse(const char* text, int64_t len, rt_obj** out) {
                         delete o;
                         return fail("line " + std::to_string(lineno) + ": bad number");
                     }
-                    (head == "v" ? o->vp : o->vn).push_back((float)v);
+                    (is_v ? o->vp : o->vn).push_back((float)v);
                 }
-            } else if (head == "vt") {
+            } else if (is_vt) {
                 double u = 0.0, v = 0.0;
                 if (ws.size() < 2 || !parse_float(ws[1].first, ws[1].second, &u) ||
                     (ws.size() > 2 && !parse_float(ws[2].first, ws[2].second, &v))) {
