@@ -425,6 +425,9 @@ __device__ Hit trace_brute(const DevScene& S, rtm_f3 o, rtm_f3 d, Cnt& c) {
 // the minimum key is the reference's hit (lowest rank on equal distances).
 // Culling uses the owner's best as of the last batch (a conservative bound).
 constexpr int BRUTE_WAVE_LDS = 64 * 6 * 4 + 64 * 8 + 128 * 2;   // ray table | best keys | pair ring
+#ifndef RT_BRUTE_UNROLL
+#define RT_BRUTE_UNROLL 1   // box-test loop unroll (several scalar record loads in flight)
+#endif
 
 // Lanes of one wave hand data to each other through LDS here.  The hardware runs a
 // wave's LDS instructions in order; this keeps the compiler from reordering them
@@ -436,7 +439,8 @@ __device__ __forceinline__ void wave_lds_sync() {
 }
 
 template <bool COUNT>
-__device__ Hit trace_brute_compact(const DevScene& S, rtm_f3 o, rtm_f3 d, char* wl, Cnt& c) {
+__device__ Hit trace_brute_compact(const DevScene& S, rtm_f3 o, rtm_f3 d, char* wl, const float4* mtrec,
+                                   unsigned mtstride, Cnt& c) {
     if (COUNT) c.rays++;
     const unsigned lane = threadIdx.x & 63;
     const unsigned long long act = __ballot(1);
@@ -460,7 +464,9 @@ __device__ Hit trace_brute_compact(const DevScene& S, rtm_f3 o, rtm_f3 d, char* 
             const unsigned ow = e >> 8, q = e & 255;
             const rtm_f3 ro = rtm_v3(ray[ow], ray[64 + ow], ray[128 + ow]);
             const rtm_f3 rd = rtm_v3(ray[192 + ow], ray[256 + ow], ray[320 + ow]);
-            const float4 r1 = S.brute[4 * q + 1], r2 = S.brute[4 * q + 2], r3 = S.brute[4 * q + 3];
+            // record q's last three float4 (hi.yz a.xy | a.z e1.xyz | e2.xyz tri): LDS copy or global
+            const float4* rq = mtrec + mtstride * q;
+            const float4 r1 = rq[0], r2 = rq[1], r3 = rq[2];
             const rtm_f3 a = rtm_v3(r1.z, r1.w, r2.x), e1 = rtm_v3(r2.y, r2.z, r2.w), e2 = rtm_v3(r3.x, r3.y, r3.z);
             const rtm_f3 h = rtm_cross(rd, e2);
             const float det = rtm_dot(e1, h);
@@ -478,6 +484,7 @@ __device__ Hit trace_brute_compact(const DevScene& S, rtm_f3 o, rtm_f3 d, char* 
         head += n;
         wave_lds_sync();
     };
+#pragma unroll RT_BRUTE_UNROLL
     for (int q = 0; q < S.nbrute; ++q) {
         if (COUNT) count_wave(c.wave_trav);
         const float4 r0 = sgpr4(S.brute[4 * q + 0]), r1 = sgpr4(S.brute[4 * q + 1]);
@@ -509,16 +516,22 @@ __device__ Hit trace_brute_compact(const DevScene& S, rtm_f3 o, rtm_f3 d, char* 
 #ifndef RT_BRUTE_COMPACT
 #define RT_BRUTE_COMPACT 1
 #endif
+#ifndef RT_BRUTE_LDS
+#define RT_BRUTE_LDS 1   // MT batches read the triangle records from an LDS copy (48 B stride)
+#endif
 
 // stk/B: the REF traversal's int stack in LDS; st: the FAST traversal's stack.
+// mtrec/mtstride: where the brute-force MT batches read triangle records (float4 units).
 template <int TRAV, bool COUNT, bool SOA = false, bool OVF = false>
 __device__ __forceinline__ Hit trace(const DevScene& S, const float4* nodes, const float4* tris, rtm_f3 o, rtm_f3 d,
-                                     int* stk, int B, const LaneStack& st, Cnt& c) {
+                                     int* stk, int B, const LaneStack& st, Cnt& c, const float4* mtrec = nullptr,
+                                     unsigned mtstride = 4) {
     if (TRAV == TRAV_REF) return trace_ref<COUNT>(S, o, d, stk, B, c);
     if (S.nbrute > 0) {
         if (RT_BRUTE_COMPACT)
             return trace_brute_compact<COUNT>(S, o, d, reinterpret_cast<char*>(stk - threadIdx.x) +
-                                                            (threadIdx.x >> 6) * BRUTE_WAVE_LDS, c);
+                                                            (threadIdx.x >> 6) * BRUTE_WAVE_LDS,
+                                              mtrec ? mtrec : S.brute + 1, mtrec ? mtstride : 4u, c);
         return trace_brute<COUNT>(S, o, d, c);
     }
     return trace_fast<COUNT, SOA, OVF>(S, nodes, tris, o, d, st, c);
@@ -774,6 +787,14 @@ __global__ void RT_RENDER_BOUNDS render_kernel(DevScene S, FrameParams F, float*
     int* stk = lds_stack + threadIdx.x;
     const LaneStack lst = lane_stack(S, lds_stack);
     Cnt c{0, 0, 0, 0, 0, 0, 0};
+    // small scenes (brute force): the MT batches' triangle records, staged behind the per-wave regions
+    const float4* mtrec = nullptr;
+    if (RT_BRUTE_COMPACT && RT_BRUTE_LDS && TRAV == TRAV_FAST && S.nbrute > 0) {
+        float4* lr = reinterpret_cast<float4*>(reinterpret_cast<char*>(lds_stack) + (B / 64) * BRUTE_WAVE_LDS);
+        for (int q = threadIdx.x; q < 3 * S.nbrute; q += B) lr[q] = S.brute[4 * (q / 3) + 1 + q % 3];
+        __syncthreads();
+        mtrec = lr;
+    }
     const LaunchConst& C = *lconst;   // uniform: scalar loads, no VGPRs
     // SMEM: the whole BVH2 node array and triangle array of a small scene are
     // staged in LDS behind the stacks, once per (persistent) block.
@@ -907,7 +928,7 @@ __global__ void RT_RENDER_BOUNDS render_kernel(DevScene S, FrameParams F, float*
         // -- one ray per busy lane --
         const rtm_f3 to = (phase == PRIMARY) ? C.position : Bo;
         const rtm_f3 td = (phase == PRIMARY) ? cd : ((phase == BOUNCE) ? Bd : C.sun);
-        const Hit h = trace<TRAV, COUNT, SMEM, OVF>(S, nodes, tris, to, td, stk, B, lst, c);
+        const Hit h = trace<TRAV, COUNT, SMEM, OVF>(S, nodes, tris, to, td, stk, B, lst, c, mtrec, 3);
         bool finish = false;
         if (phase == PRIMARY) {
             tc = h.tri;
@@ -1301,7 +1322,7 @@ hipError_t launch_t(const DevScene& sc, const FrameParams& fp, int block, float*
     const int depth = (TRAV == TRAV_REF) ? REF_STACK : (sc.nbrute > 0 ? 1 : 2 * (sc.stack_lds > 0 ? sc.stack_lds : 1));
     size_t lds = (size_t)depth * block * sizeof(int);
     if (TRAV == TRAV_FAST && sc.nbrute > 0 && RT_BRUTE_COMPACT)
-        lds = std::max(lds, (size_t)(block / 64) * BRUTE_WAVE_LDS);
+        lds = std::max(lds, (size_t)(block / 64) * BRUTE_WAVE_LDS + (RT_BRUTE_LDS ? (size_t)sc.nbrute * 48 : 0));
     if (SMEM) lds += (size_t)(kNodeF4 * sc.nnodes + 3 * sc.ntri) * sizeof(float4);
     const int64_t need = (fp.nloc + block - 1) / block;
     if (need <= 0) return hipSuccess;
