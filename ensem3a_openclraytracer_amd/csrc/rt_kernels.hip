@@ -777,7 +777,7 @@ enum Phase { FETCH = 0, PRIMARY = 1, PREP = 2, BOUNCE = 3, SUN = 4, DONE = 5 };
 // base + (its rank among the requesting lanes) -- so no lane idles while the
 // rest of its wave finishes a slower pixel.  Per loop iteration every busy
 // lane traces exactly one ray (primary, bounce or sun ray).
-template <int TRAV, bool COUNT, bool LOG = false, bool SMEM = false, bool OVF = false>
+template <int TRAV, bool COUNT, bool LOG = false, bool SMEM = false, bool OVF = false, bool BRUTE = false>
 __global__ void RT_RENDER_BOUNDS render_kernel(DevScene S, FrameParams F, float* __restrict__ out,
                                                unsigned long long* __restrict__ counts,
                                                unsigned int* __restrict__ work_counter,
@@ -787,13 +787,26 @@ __global__ void RT_RENDER_BOUNDS render_kernel(DevScene S, FrameParams F, float*
     int* stk = lds_stack + threadIdx.x;
     const LaneStack lst = lane_stack(S, lds_stack);
     Cnt c{0, 0, 0, 0, 0, 0, 0};
-    // small scenes (brute force): the MT batches' triangle records, staged behind the per-wave regions
+    // BRUTE (small scenes, brute-force traversal): the MT batches' triangle records and all shading
+    // tables (hit records, hemisphere frames, materials) are staged in LDS behind the per-wave regions
     const float4* mtrec = nullptr;
-    if (RT_BRUTE_COMPACT && RT_BRUTE_LDS && TRAV == TRAV_FAST && S.nbrute > 0) {
+    const float4* tshade = S.tri_shade;
+    const float4* tframe = S.tri_frame;
+    const float* tmat = S.mat;
+    if (BRUTE) {
         float4* lr = reinterpret_cast<float4*>(reinterpret_cast<char*>(lds_stack) + (B / 64) * BRUTE_WAVE_LDS);
+        float4* ls = lr + 3 * S.nbrute;
+        float4* lf = ls + S.ntri;
+        float* lm = reinterpret_cast<float*>(lf + 3 * S.ntri);
         for (int q = threadIdx.x; q < 3 * S.nbrute; q += B) lr[q] = S.brute[4 * (q / 3) + 1 + q % 3];
+        for (int q = threadIdx.x; q < S.ntri; q += B) ls[q] = S.tri_shade[q];
+        for (int q = threadIdx.x; q < 3 * S.ntri; q += B) lf[q] = S.tri_frame[q];
+        for (int q = threadIdx.x; q < 6 * S.nmat; q += B) lm[q] = S.mat[q];
         __syncthreads();
         mtrec = lr;
+        tshade = ls;
+        tframe = lf;
+        tmat = lm;
     }
     const LaunchConst& C = *lconst;   // uniform: scalar loads, no VGPRs
     // SMEM: the whole BVH2 node array and triangle array of a small scene are
@@ -876,22 +889,22 @@ __global__ void RT_RENDER_BOUNDS render_kernel(DevScene S, FrameParams F, float*
             } else if (tri < 0) {
                 so = rtm_scale(rtm_mul(so, sample_ibl_if<COUNT>(S, C, Rd, e4, c)), e4);
             } else {
-                const float4 sh = S.tri_shade[tri];
+                const float4 sh = tshade[tri];
                 const rtm_f3 n = xyz(sh);
-                const Mat cm = load_mat(S.mat, __float_as_int(sh.w));
+                const Mat cm = load_mat(tmat, __float_as_int(sh.w));
                 if (cm.type == 0) {
                     so = rtm_scale(so, cm.rough);
                 } else {
-                    const float4 f2 = S.tri_frame[3 * tri + 2];
+                    const float4 f2 = tframe[3 * tri + 2];
                     const rtm_f3 nn = xyz(f2);
                     float invPdf = 0.0f;
                     rtm_f3 brdf = rtm_v3(0, 0, 0);
                     if (cm.type == 1) {
-                        Bd = hemi_cosine(n, S.tri_frame[3 * tri], S.tri_frame[3 * tri + 1], f2, &seed1, &seed0,
+                        Bd = hemi_cosine(n, tframe[3 * tri], tframe[3 * tri + 1], f2, &seed1, &seed0,
                                          &invPdf);
                         brdf = rtm_scale(cm.color, 1.0f / 3.14f);
                     } else if (cm.type == 2) {
-                        Bd = hemi_uniform(n, S.tri_frame[3 * tri], S.tri_frame[3 * tri + 1], f2, &seed1, &seed0,
+                        Bd = hemi_uniform(n, tframe[3 * tri], tframe[3 * tri + 1], f2, &seed1, &seed0,
                                           &invPdf);
                         brdf = brdf_ggx(cm.color, cm.rough, rtm_scale(Rd, -1.0f), Bd, n);
                     } else {
@@ -943,13 +956,13 @@ __global__ void RT_RENDER_BOUNDS render_kernel(DevScene S, FrameParams F, float*
             continue;
         }
         if (LOG && logme) {
-            const int hm = h.tri >= 0 ? __float_as_int(S.tri_shade[h.tri].w) : 0;
+            const int hm = h.tri >= 0 ? __float_as_int(tshade[h.tri].w) : 0;
             log_event(F, phase == BOUNCE ? 1.0f : 2.0f, j, Bo, td, h.tri >= 0 ? h.k : -1.0f, hm, so);
         }
         if (phase == BOUNCE) {
             if (h.tri >= 0) {
                 Ro = Bo; Rd = Bd; tri = h.tri; k = h.k;
-                const Mat bm = load_mat(S.mat, __float_as_int(S.tri_shade[h.tri].w));
+                const Mat bm = load_mat(tmat, __float_as_int(tshade[h.tri].w));
                 if (bm.type != 0) {
                     if (j == maxB) {
                         so = rtm_v3(0, 0, 0);
@@ -967,10 +980,10 @@ __global__ void RT_RENDER_BOUNDS render_kernel(DevScene S, FrameParams F, float*
             }
         } else {  // SUN (Raytracing.cl:115-137)
             rtm_f3 sunLight = rtm_v3(0, 0, 0);
-            const Mat cm = load_mat(S.mat, __float_as_int(S.tri_shade[tri].w));
+            const Mat cm = load_mat(tmat, __float_as_int(tshade[tri].w));
             if (h.tri < 0 && cm.type != 3) sunLight = rtm_v3(e3, e3, e3);
             if (h.tri >= 0) {
-                const Mat sm = load_mat(S.mat, __float_as_int(S.tri_shade[h.tri].w));
+                const Mat sm = load_mat(tmat, __float_as_int(tshade[h.tri].w));
                 if (sm.type == 3) sunLight = rtm_scale(sm.color, e3);
             }
             const rtm_f3 envLight = rtm_scale(sample_ibl_if<COUNT>(S, C, Bd, e4, c), e4);
@@ -1315,14 +1328,18 @@ __global__ void gamma_kernel(const float* __restrict__ in, float* __restrict__ o
     }
 }
 
-template <int TRAV, bool COUNT, bool LOG, bool SMEM = false, bool RESUME = false, bool OVF = false>
+template <int TRAV, bool COUNT, bool LOG, bool SMEM = false, bool RESUME = false, bool OVF = false,
+          bool BRUTE = false>
 hipError_t launch_t(const DevScene& sc, const FrameParams& fp, int block, float* d_out, unsigned long long* d_counts,
                     unsigned int* d_work, hipStream_t stream) {
     // FAST: int2 entries; the brute-force path of small scenes needs no stack
     const int depth = (TRAV == TRAV_REF) ? REF_STACK : (sc.nbrute > 0 ? 1 : 2 * (sc.stack_lds > 0 ? sc.stack_lds : 1));
     size_t lds = (size_t)depth * block * sizeof(int);
     if (TRAV == TRAV_FAST && sc.nbrute > 0 && RT_BRUTE_COMPACT)
-        lds = std::max(lds, (size_t)(block / 64) * BRUTE_WAVE_LDS + (RT_BRUTE_LDS ? (size_t)sc.nbrute * 48 : 0));
+        lds = std::max(lds, (size_t)(block / 64) * BRUTE_WAVE_LDS);
+    if (BRUTE)
+        lds = (size_t)(block / 64) * BRUTE_WAVE_LDS + (size_t)sc.nbrute * 48 + (size_t)sc.ntri * 64 +
+              (size_t)sc.nmat * 24;
     if (SMEM) lds += (size_t)(kNodeF4 * sc.nnodes + 3 * sc.ntri) * sizeof(float4);
     const int64_t need = (fp.nloc + block - 1) / block;
     if (need <= 0) return hipSuccess;
@@ -1331,7 +1348,7 @@ hipError_t launch_t(const DevScene& sc, const FrameParams& fp, int block, float*
     hipError_t e = hipGetDevice(&dev);
     if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     const void* kfn = RESUME ? (const void*)render_resume_kernel<COUNT, LOG, SMEM, OVF>
-                             : (const void*)render_kernel<TRAV, COUNT, LOG, SMEM, OVF>;
+                             : (const void*)render_kernel<TRAV, COUNT, LOG, SMEM, OVF, BRUTE>;
     if (e == hipSuccess) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kfn, block, lds);
     if (e != hipSuccess) return e;
     const int64_t resident = (int64_t)std::max(1, cus) * std::max(1, per_cu);
@@ -1345,7 +1362,8 @@ hipError_t launch_t(const DevScene& sc, const FrameParams& fp, int block, float*
         hipLaunchKernelGGL((render_resume_kernel<COUNT, LOG, SMEM, OVF>), dim3((unsigned)grid), dim3(block), lds, stream,
                            sc, fp, d_out, d_counts, d_work, (const LaunchConst*)lc);
     else
-        hipLaunchKernelGGL((render_kernel<TRAV, COUNT, LOG, SMEM, OVF>), dim3((unsigned)grid), dim3(block), lds, stream,
+        hipLaunchKernelGGL((render_kernel<TRAV, COUNT, LOG, SMEM, OVF, BRUTE>), dim3((unsigned)grid), dim3(block), lds,
+                           stream,
                            sc, fp, d_out, d_counts, d_work, (const LaunchConst*)lc);
     return hipGetLastError();
 }
@@ -1443,6 +1461,9 @@ hipError_t launch_fast(const DevScene& sc, const FrameParams& fp, int block, flo
                                                                           stream);
         return launch_t<TRAV_FAST, COUNT, false, false, true>(sc, fp, block, d_out, d_counts, d_work, stream);
     }
+    if (sc.ntri > 0 && sc.nbrute > 0 && RT_BRUTE_COMPACT && RT_BRUTE_LDS && sc.ntri <= 1024)
+        return launch_t<TRAV_FAST, COUNT, false, false, false, false, true>(sc, fp, block, d_out, d_counts, d_work,
+                                                                            stream);
     if (smem) return launch_t<TRAV_FAST, COUNT, false, true>(sc, fp, block, d_out, d_counts, d_work, stream);
     if (ovf)
         return launch_t<TRAV_FAST, COUNT, false, false, false, true>(sc, fp, block, d_out, d_counts, d_work, stream);
