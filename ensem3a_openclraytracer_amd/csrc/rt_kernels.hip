@@ -369,6 +369,19 @@ __device__ Hit trace_fast(const DevScene& S, const float4* __restrict__ nodes, c
 // hit, k > 1e-4), and records are in the reference's DFS order, so the strict
 // `<` keeps the lowest rank on equal distances: the same hit as trace_fast.
 // Record (4 x float4): lo.xyz hi.x | hi.yz a.xy | a.z e1.xyz | e2.xyz tri.
+// Read-only data read through the constant address space: wave-uniform addresses become scalar
+// loads (s_load_*) whatever the surrounding control flow.
+typedef const float __attribute__((address_space(4))) const_f;
+struct ConstF4 {
+    const const_f* p;
+    __device__ __forceinline__ float4 operator[](int i) const {
+        return make_float4(p[4 * i], p[4 * i + 1], p[4 * i + 2], p[4 * i + 3]);
+    }
+};
+__device__ __forceinline__ ConstF4 as_const(const float4* p) {
+    return ConstF4{(const const_f*)(const float*)(p)};   // C-style: an address-space cast
+}
+
 __device__ __forceinline__ float sgpr1(float x) {
     return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(x)));
 }
@@ -386,8 +399,9 @@ __device__ Hit trace_brute(const DevScene& S, rtm_f3 o, rtm_f3 d, Cnt& c) {
         if (COUNT) count_wave(c.wave_trav);
         // the record is wave-uniform: readfirstlane pins it in SGPRs (one s_load_dwordx16, SGPR
         // operands).  Prefetching the next record costs more SALU moves than the latency it hides.
-        const float4 r0 = sgpr4(S.brute[4 * q + 0]), r1 = sgpr4(S.brute[4 * q + 1]);
-        const float4 r2 = sgpr4(S.brute[4 * q + 2]), r3 = sgpr4(S.brute[4 * q + 3]);
+        const ConstF4 cb = as_const(S.brute);
+        const float4 r0 = sgpr4(cb[4 * q + 0]), r1 = sgpr4(cb[4 * q + 1]);
+        const float4 r2 = sgpr4(cb[4 * q + 2]), r3 = sgpr4(cb[4 * q + 3]);
         float tn, tx;
         slab_fma(r0.x, r0.w, r0.y, r1.x, r0.z, r1.y, o.x, o.y, o.z, ix, iy, iz, oix, oiy, oiz, tn, tx);
         const bool pass = fmaxf(tn, 0.0f) <= fminf(tx, best.k * CULL_MARGIN);
@@ -487,7 +501,8 @@ __device__ Hit trace_brute_compact(const DevScene& S, rtm_f3 o, rtm_f3 d, char* 
 #pragma unroll RT_BRUTE_UNROLL
     for (int q = 0; q < S.nbrute; ++q) {
         if (COUNT) count_wave(c.wave_trav);
-        const float4 r0 = sgpr4(S.brute[4 * q + 0]), r1 = sgpr4(S.brute[4 * q + 1]);
+        const ConstF4 cb = as_const(S.brute);
+        const float4 r0 = sgpr4(cb[4 * q + 0]), r1 = sgpr4(cb[4 * q + 1]);
         float tn, tx;
         slab_fma(r0.x, r0.w, r0.y, r1.x, r0.z, r1.y, o.x, o.y, o.z, ix, iy, iz, oix, oiy, oiz, tn, tx);
         const bool pass = fmaxf(tn, 0.0f) <= fminf(tx, bk * CULL_MARGIN);
@@ -522,16 +537,17 @@ __device__ Hit trace_brute_compact(const DevScene& S, rtm_f3 o, rtm_f3 d, char* 
 
 // stk/B: the REF traversal's int stack in LDS; st: the FAST traversal's stack.
 // mtrec/mtstride: where the brute-force MT batches read triangle records (float4 units).
-template <int TRAV, bool COUNT, bool SOA = false, bool OVF = false>
+// BLDS: the caller staged the MT records in LDS at mtrec (3 float4 per triangle); otherwise they
+// are read from the global brute-force records.
+template <int TRAV, bool COUNT, bool SOA = false, bool OVF = false, bool BLDS = false>
 __device__ __forceinline__ Hit trace(const DevScene& S, const float4* nodes, const float4* tris, rtm_f3 o, rtm_f3 d,
-                                     int* stk, int B, const LaneStack& st, Cnt& c, const float4* mtrec = nullptr,
-                                     unsigned mtstride = 4) {
+                                     int* stk, int B, const LaneStack& st, Cnt& c, const float4* mtrec = nullptr) {
     if (TRAV == TRAV_REF) return trace_ref<COUNT>(S, o, d, stk, B, c);
     if (S.nbrute > 0) {
         if (RT_BRUTE_COMPACT)
             return trace_brute_compact<COUNT>(S, o, d, reinterpret_cast<char*>(stk - threadIdx.x) +
                                                             (threadIdx.x >> 6) * BRUTE_WAVE_LDS,
-                                              mtrec ? mtrec : S.brute + 1, mtrec ? mtstride : 4u, c);
+                                              BLDS ? mtrec : S.brute + 1, BLDS ? 3u : 4u, c);
         return trace_brute<COUNT>(S, o, d, c);
     }
     return trace_fast<COUNT, SOA, OVF>(S, nodes, tris, o, d, st, c);
@@ -941,7 +957,7 @@ __global__ void RT_RENDER_BOUNDS render_kernel(DevScene S, FrameParams F, float*
         // -- one ray per busy lane --
         const rtm_f3 to = (phase == PRIMARY) ? C.position : Bo;
         const rtm_f3 td = (phase == PRIMARY) ? cd : ((phase == BOUNCE) ? Bd : C.sun);
-        const Hit h = trace<TRAV, COUNT, SMEM, OVF>(S, nodes, tris, to, td, stk, B, lst, c, mtrec, 3);
+        const Hit h = trace<TRAV, COUNT, SMEM, OVF, BRUTE>(S, nodes, tris, to, td, stk, B, lst, c, mtrec);
         bool finish = false;
         if (phase == PRIMARY) {
             tc = h.tri;
