@@ -16,7 +16,10 @@ Extra fields:
                   (this build's own traversal counters x bytes per unit, see
                   DESIGN.md) / average kernel time from HIP events on the launch
                   stream; peak = 8 TB/s HBM; traffic = PMC-measured HBM bytes per
-                  launch from profiles/ (rocprofv3) when present, else null.
+                  launch from profiles/ (rocprofv3) when present, else null;
+                  traffic_frac = that measured traffic / kernel time / peak.  On a
+                  cache-resident scene (C2) frac > 1: the algorithmic bytes are
+                  served from LDS / scalar cache / L2, not HBM.
   cpu_baseline -- the CPU oracle (a C restatement of the reference kernel, OpenMP)
                   timed on this host on a bounded row sample of the same frame.
 """
@@ -199,6 +202,7 @@ def main():
         ms_per_step = elapsed / args.steps * 1e3
         value = samples * args.steps / elapsed / 1e6
         achieved = alg_bytes / (kernel_ms * 1e-3) / 1e9
+        traffic = _pmc_traffic(wl.name)   # measured HBM bytes per launch (committed rocprofv3 PMC summary)
         line = {
             "metric": METRIC, "value": round(value, 3), "unit": "Msamples/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4),
@@ -209,7 +213,9 @@ def main():
                        "parallelism": f"row-interleaved x{world}" + (
                            (" + gloo gather (one-GPU rehearsal)" if rehearsal else " + RCCL gather") if world > 1 else "")},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": _pmc_traffic(wl.name),
+                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                         "traffic_frac": (round(traffic / (kernel_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 5)
+                                          if traffic else None),
                          "kernel_ms": round(kernel_ms, 4), "alg_bytes_per_launch": int(alg_bytes),
                          "bytes_model": "SURVEY 8(d): 32 B/box tested (FAST node = 2 boxes), 36 B/triangle test, "
                                         "40 B/ray hit record, 16 B/IBL lookup; counts of this build's SAH tree walk",
