@@ -232,11 +232,11 @@ class Context:
     def wave_counts(self, cam, env, npix, spp, max_bounce):
         """rt_debug_wave_counts: lane counters + wave-level loop iterations of one frame."""
         c, e = f32(cam), f32(env)
-        out = np.zeros(7, dtype=np.uint64)
+        out = np.zeros(9, dtype=np.uint64)
         self._check(lib().rt_debug_wave_counts(self.handle, ptr(c), ptr(e), int(npix), int(spp), int(max_bounce),
                                                out.ctypes.data))
         keys = ("node_fetches", "tri_tests", "rays", "env_lookups", "stack_drops", "wave_trav_iters",
-                "wave_render_iters")
+                "wave_render_iters", "cycles_shade", "cycles_trav")
         return {k: int(v) for k, v in zip(keys, out)}
 
     def scene_info(self):

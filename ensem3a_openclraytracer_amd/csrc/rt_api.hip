@@ -75,6 +75,7 @@ struct rt_ctx {
     int bvh_layout = RT_BVH_SAH;
     int brute_max = RT_BRUTE_MAX_DEFAULT;
     int resume_min = RT_RESUME_MIN_DEFAULT;
+    int team = 0;  // brute-force lanes per pixel, 0 = auto
     int block = 128;
     std::string err;
 };
@@ -414,6 +415,7 @@ int check_frame(rt_ctx* ctx, const float* cam, const float* env, int64_t npix, i
     fp->nloc = rt_tile_rows(npix, fp->width, row0, row_step) * fp->width;
     fp->log_pixel = -1;
     fp->resume_min = ctx->resume_min;
+    fp->team = ctx->team;
     fp->log_buf = nullptr;
     fp->log_cap = 0;
     fp->log_count = nullptr;
@@ -515,6 +517,12 @@ int rt_set_option(rt_ctx* ctx, const char* key, int64_t value) {
     if (!std::strcmp(key, "resume_min")) {
         if (value < 0 || value > 64) return set_err(ctx, RT_ERR_ARG, "resume_min must be in 0..64");
         ctx->resume_min = (int)value;
+        return RT_OK;
+    }
+    if (!std::strcmp(key, "team")) {
+        if (value != 0 && value != 1 && value != 2 && value != 4 && value != 8)
+            return set_err(ctx, RT_ERR_ARG, "team must be 0 (auto), 1, 2, 4 or 8");
+        ctx->team = (int)value;
         return RT_OK;
     }
     if (!std::strcmp(key, "block")) {
@@ -734,7 +742,7 @@ int count_all(rt_ctx* ctx, const float cam[10], const float env[5], int64_t npix
     HIP_OR_RET(ctx, hipSetDevice(d.id));
     const size_t bytes = (size_t)fp.nloc * 3 * sizeof(float);
     HIP_OR_RET(ctx, ensure(d.out, bytes > 0 ? bytes : 16));
-    unsigned long long h[8] = {0};
+    unsigned long long h[16] = {0};
     HIP_OR_RET(ctx, ensure(d.counts, sizeof h));
     HIP_OR_RET(ctx, hipMemsetAsync(d.counts.p, 0, sizeof h, d.stream));
     HIP_OR_RET(ctx, rt::launch_render(dev_scene(ctx, d), fp, effective_traversal(ctx), ctx->block, (float*)d.out.p,
@@ -752,8 +760,8 @@ int rt_count_work(rt_ctx* ctx, const float cam[10], const float env[5], int64_t 
 }
 
 int rt_debug_wave_counts(rt_ctx* ctx, const float cam[10], const float env[5], int64_t npix, int spp, int max_bounce,
-                         uint64_t counts[7]) {
-    return count_all(ctx, cam, env, npix, spp, max_bounce, 0, 1, counts, 7);
+                         uint64_t counts[9]) {
+    return count_all(ctx, cam, env, npix, spp, max_bounce, 0, 1, counts, 9);
 }
 
 int rt_work_bytes(rt_ctx* ctx, double out[4]) {

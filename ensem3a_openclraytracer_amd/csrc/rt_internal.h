@@ -66,6 +66,7 @@ struct FrameParams {
     int32_t row0, row_step;
     int64_t nloc;        // pixels in this tile = rows * width
     int32_t resume_min;  // FAST tree walk: resumable traversal, shade once this many lanes are free (0 = off)
+    int32_t team;        // brute-force path: lanes per pixel (1, 2, 4, 8; 0 = chosen at launch from the tile size)
     // debug event log of one pixel (rt_debug_pixel_log only; unused by the product launches)
     int64_t log_pixel;
     float* log_buf;

@@ -52,8 +52,10 @@ struct Cnt {
     unsigned long long nodes, tris, rays, env, dropped;
     unsigned long long wave_trav;   // traversal-loop iterations issued per wave (any lane active)
     unsigned long long wave_outer;  // render-loop iterations per wave
+    unsigned long long cyc_shade;   // resumable kernel, per wave: clock cycles outside the traversal rounds
+    unsigned long long cyc_trav;    //   ... and inside them
 };
-constexpr int NCOUNTS = 7;
+constexpr int NCOUNTS = 9;
 
 // COUNT builds: the lowest active lane of the wave counts one wave-level iteration.
 __device__ __forceinline__ void count_wave(unsigned long long& x) {
@@ -438,7 +440,7 @@ __device__ Hit trace_brute(const DevScene& S, rtm_f3 o, rtm_f3 d, Cnt& c) {
 // (distance bits, DFS position): positive float bits order like the floats, so
 // the minimum key is the reference's hit (lowest rank on equal distances).
 // Culling uses the owner's best as of the last batch (a conservative bound).
-constexpr int BRUTE_WAVE_LDS = 64 * 6 * 4 + 64 * 8 + 128 * 2;   // ray table | best keys | pair ring
+constexpr int BRUTE_WAVE_LDS = 64 * 6 * 4 + 64 * 8 + 128 * 4;   // ray table | best keys | pair ring
 #ifndef RT_BRUTE_UNROLL
 #define RT_BRUTE_UNROLL 1   // box-test loop unroll (several scalar record loads in flight)
 #endif
@@ -453,16 +455,21 @@ __device__ __forceinline__ void wave_lds_sync() {
 }
 
 template <bool COUNT>
+// Teams (ts = 2 or 4 lanes per pixel, when a tile has fewer pixels than the GPU has lanes): the
+// ts lanes of a team carry the same path (identical arithmetic), split the box tests between
+// them (lane `sub` of the team tests records sub, sub + ts, ...; records read from the LDS copy
+// at boxrec, 1 float4 per triangle, and mtrec) and share one owner slot (the team's first lane).
 __device__ Hit trace_brute_compact(const DevScene& S, rtm_f3 o, rtm_f3 d, char* wl, const float4* mtrec,
-                                   unsigned mtstride, Cnt& c) {
-    if (COUNT) c.rays++;
+                                   unsigned mtstride, Cnt& c, int ts = 1, const float4* boxrec = nullptr) {
     const unsigned lane = threadIdx.x & 63;
+    const unsigned sub = lane & (unsigned)(ts - 1), tl = lane - sub;   // lane in team, team leader
+    if (COUNT && sub == 0) c.rays++;
     const unsigned long long act = __ballot(1);
     const int nact = __popcll(act);
     const int myrank = __popcll(act & ((1ull << lane) - 1ull));
     float* ray = reinterpret_cast<float*>(wl);                                   // [6][64]
     unsigned long long* bestk = reinterpret_cast<unsigned long long*>(wl + 64 * 6 * 4);
-    unsigned short* ring = reinterpret_cast<unsigned short*>(wl + 64 * 6 * 4 + 64 * 8);
+    unsigned* ring = reinterpret_cast<unsigned*>(wl + 64 * 6 * 4 + 64 * 8);   // owner << 16 | triangle
     ray[0 * 64 + lane] = o.x; ray[1 * 64 + lane] = o.y; ray[2 * 64 + lane] = o.z;
     ray[3 * 64 + lane] = d.x; ray[4 * 64 + lane] = d.y; ray[5 * 64 + lane] = d.z;
     const unsigned long long nokey = ((unsigned long long)__float_as_uint(1000.0f) << 32) | 0xffffffffull;
@@ -475,7 +482,7 @@ __device__ Hit trace_brute_compact(const DevScene& S, rtm_f3 o, rtm_f3 d, char* 
     auto run_batch = [&](int n) __attribute__((always_inline)) {
         if (myrank < n) {
             const unsigned e = ring[(head + myrank) & 127];
-            const unsigned ow = e >> 8, q = e & 255;
+            const unsigned ow = e >> 16, q = e & 0xffffu;
             const rtm_f3 ro = rtm_v3(ray[ow], ray[64 + ow], ray[128 + ow]);
             const rtm_f3 rd = rtm_v3(ray[192 + ow], ray[256 + ow], ray[320 + ow]);
             // record q's last three float4 (hi.yz a.xy | a.z e1.xyz | e2.xyz tri): LDS copy or global
@@ -498,28 +505,49 @@ __device__ Hit trace_brute_compact(const DevScene& S, rtm_f3 o, rtm_f3 d, char* 
         head += n;
         wave_lds_sync();
     };
-#pragma unroll RT_BRUTE_UNROLL
-    for (int q = 0; q < S.nbrute; ++q) {
-        if (COUNT) count_wave(c.wave_trav);
-        const ConstF4 cb = as_const(S.brute);
-        const float4 r0 = sgpr4(cb[4 * q + 0]), r1 = sgpr4(cb[4 * q + 1]);
-        float tn, tx;
-        slab_fma(r0.x, r0.w, r0.y, r1.x, r0.z, r1.y, o.x, o.y, o.z, ix, iy, iz, oix, oiy, oiz, tn, tx);
-        const bool pass = fmaxf(tn, 0.0f) <= fminf(tx, bk * CULL_MARGIN);
-        if (COUNT) c.nodes++;
+    // queue a passing (owner, triangle) pair; run a batch once a full wave of pairs is queued
+    auto enqueue = [&](bool pass, unsigned q) __attribute__((always_inline)) {
         const unsigned long long m = __ballot(pass);
-        if (m == 0) continue;
+        if (m == 0) return;
         if (COUNT && pass) c.tris++;
-        if (pass) ring[(tail + __popcll(m & ((1ull << lane) - 1ull))) & 127] = (unsigned short)((lane << 8) | q);
+        if (pass) ring[(tail + __popcll(m & ((1ull << lane) - 1ull))) & 127] = (tl << 16) | q;
         tail += __popcll(m);
         wave_lds_sync();
         if ((int)(tail - head) >= nact) {
             run_batch(nact);
-            bk = __uint_as_float((unsigned)(bestk[lane] >> 32));
+            bk = __uint_as_float((unsigned)(bestk[tl] >> 32));
+        }
+    };
+    if (ts == 1) {
+#pragma unroll RT_BRUTE_UNROLL
+        for (int q = 0; q < S.nbrute; ++q) {
+            if (COUNT) count_wave(c.wave_trav);
+            const ConstF4 cb = as_const(S.brute);
+            const float4 r0 = sgpr4(cb[4 * q + 0]), r1 = sgpr4(cb[4 * q + 1]);
+            float tn, tx;
+            slab_fma(r0.x, r0.w, r0.y, r1.x, r0.z, r1.y, o.x, o.y, o.z, ix, iy, iz, oix, oiy, oiz, tn, tx);
+            const bool pass = fmaxf(tn, 0.0f) <= fminf(tx, bk * CULL_MARGIN);
+            if (COUNT) c.nodes++;
+            enqueue(pass, (unsigned)q);
+        }
+    } else {
+        const int rounds = (S.nbrute + ts - 1) / ts;
+        for (int qq = 0; qq < rounds; ++qq) {
+            if (COUNT) count_wave(c.wave_trav);
+            const int q = qq * ts + (int)sub;
+            bool pass = false;
+            if (q < S.nbrute) {
+                const float4 r0 = boxrec[q], r1 = mtrec[mtstride * q];
+                float tn, tx;
+                slab_fma(r0.x, r0.w, r0.y, r1.x, r0.z, r1.y, o.x, o.y, o.z, ix, iy, iz, oix, oiy, oiz, tn, tx);
+                pass = fmaxf(tn, 0.0f) <= fminf(tx, bk * CULL_MARGIN);
+                if (COUNT) c.nodes++;
+            }
+            enqueue(pass, (unsigned)q);
         }
     }
     while (tail != head) run_batch(min((int)(tail - head), nact));
-    const unsigned long long key = bestk[lane];
+    const unsigned long long key = bestk[tl];
     Hit best{1000.0f, -1};
     if (key != nokey) {
         best.k = __uint_as_float((unsigned)(key >> 32));
@@ -541,13 +569,15 @@ __device__ Hit trace_brute_compact(const DevScene& S, rtm_f3 o, rtm_f3 d, char* 
 // are read from the global brute-force records.
 template <int TRAV, bool COUNT, bool SOA = false, bool OVF = false, bool BLDS = false>
 __device__ __forceinline__ Hit trace(const DevScene& S, const float4* nodes, const float4* tris, rtm_f3 o, rtm_f3 d,
-                                     int* stk, int B, const LaneStack& st, Cnt& c, const float4* mtrec = nullptr) {
+                                     int* stk, int B, const LaneStack& st, Cnt& c, const float4* mtrec = nullptr,
+                                     int ts = 1, const float4* boxrec = nullptr) {
     if (TRAV == TRAV_REF) return trace_ref<COUNT>(S, o, d, stk, B, c);
     if (S.nbrute > 0) {
         if (RT_BRUTE_COMPACT)
             return trace_brute_compact<COUNT>(S, o, d, reinterpret_cast<char*>(stk - threadIdx.x) +
                                                             (threadIdx.x >> 6) * BRUTE_WAVE_LDS,
-                                              BLDS ? mtrec : S.brute + 1, BLDS ? 3u : 4u, c);
+                                              BLDS ? mtrec : S.brute + 1, BLDS ? 3u : 4u, c, BLDS ? ts : 1,
+                                              boxrec);
         return trace_brute<COUNT>(S, o, d, c);
     }
     return trace_fast<COUNT, SOA, OVF>(S, nodes, tris, o, d, st, c);
@@ -802,16 +832,20 @@ __global__ void RT_RENDER_BOUNDS render_kernel(DevScene S, FrameParams F, float*
     const int B = blockDim.x;
     int* stk = lds_stack + threadIdx.x;
     const LaneStack lst = lane_stack(S, lds_stack);
-    Cnt c{0, 0, 0, 0, 0, 0, 0};
+    Cnt c{0, 0, 0, 0, 0, 0, 0, 0, 0};
     // BRUTE (small scenes, brute-force traversal): the MT batches' triangle records and all shading
     // tables (hit records, hemisphere frames, materials) are staged in LDS behind the per-wave regions
     const float4* mtrec = nullptr;
+    const float4* boxrec = nullptr;
     const float4* tshade = S.tri_shade;
     const float4* tframe = S.tri_frame;
     const float* tmat = S.mat;
     if (BRUTE) {
         float4* lr = reinterpret_cast<float4*>(reinterpret_cast<char*>(lds_stack) + (B / 64) * BRUTE_WAVE_LDS);
-        float4* ls = lr + 3 * S.nbrute;
+        float4* lb = lr + 3 * S.nbrute;                  // lo.xyz hi.x of each record (team box tests)
+        for (int q = threadIdx.x; q < S.nbrute; q += B) lb[q] = S.brute[4 * q];
+        boxrec = lb;
+        float4* ls = lb + S.nbrute;
         float4* lf = ls + S.ntri;
         float* lm = reinterpret_cast<float*>(lf + 3 * S.ntri);
         for (int q = threadIdx.x; q < 3 * S.nbrute; q += B) lr[q] = S.brute[4 * (q / 3) + 1 + q % 3];
@@ -845,6 +879,11 @@ __global__ void RT_RENDER_BOUNDS render_kernel(DevScene S, FrameParams F, float*
     const int spp = F.spp, maxB = F.max_bounce;
     const unsigned int nloc = (unsigned int)F.nloc;
     const int lane = threadIdx.x & 63;
+    const int ts = BRUTE ? F.team : 1;                           // lanes per pixel (1, 2, 4, 8)
+    const int team_lane0 = lane & ~(ts - 1);
+    const bool team_leader = lane == team_lane0;
+    const unsigned long long team_leaders = ts == 1 ? ~0ull : ts == 2 ? 0x5555555555555555ull
+                                             : ts == 4 ? 0x1111111111111111ull : 0x0101010101010101ull;
 
     int phase = FETCH;
     int p = 0, i = 0;
@@ -862,14 +901,15 @@ __global__ void RT_RENDER_BOUNDS render_kernel(DevScene S, FrameParams F, float*
 
     while (true) {
         // -- refill: ballot the lanes that need a pixel, one atomic per wave --
-        const unsigned long long need = __ballot(phase == FETCH);
+        // teams (BRUTE, F.team lanes per pixel): one bit per team, the team's lanes take the same pixel
+        const unsigned long long need = __ballot(phase == FETCH) & team_leaders;
         if (need) {
             unsigned int base = 0;
             const int leader = __ffsll((long long)need) - 1;
             if (lane == leader) base = atomicAdd(work_counter, (unsigned int)__popcll(need));
             base = __shfl(base, leader, 64);
             if (phase == FETCH) {
-                const unsigned long long below = need & ((1ull << lane) - 1ull);
+                const unsigned long long below = need & ((1ull << team_lane0) - 1ull);
                 const unsigned int q = base + (unsigned int)__popcll(below);
                 bool ok = q < nloc;
                 if (ok) {
@@ -948,7 +988,7 @@ __global__ void RT_RENDER_BOUNDS render_kernel(DevScene S, FrameParams F, float*
                     so = rtm_v3(1, 1, 1);
                 }
                 if (phase == FETCH) {
-                    store_pixel(out, p, acc, spp);
+                    if (team_leader) store_pixel(out, p, acc, spp);
                 }
                 continue;
             }
@@ -957,7 +997,7 @@ __global__ void RT_RENDER_BOUNDS render_kernel(DevScene S, FrameParams F, float*
         // -- one ray per busy lane --
         const rtm_f3 to = (phase == PRIMARY) ? C.position : Bo;
         const rtm_f3 td = (phase == PRIMARY) ? cd : ((phase == BOUNCE) ? Bd : C.sun);
-        const Hit h = trace<TRAV, COUNT, SMEM, OVF, BRUTE>(S, nodes, tris, to, td, stk, B, lst, c, mtrec);
+        const Hit h = trace<TRAV, COUNT, SMEM, OVF, BRUTE>(S, nodes, tris, to, td, stk, B, lst, c, mtrec, ts, boxrec);
         bool finish = false;
         if (phase == PRIMARY) {
             tc = h.tri;
@@ -966,7 +1006,7 @@ __global__ void RT_RENDER_BOUNDS render_kernel(DevScene S, FrameParams F, float*
             so = rtm_v3(1, 1, 1);
             phase = PREP;
             if (spp <= 0) {   // reference: output = 0/0 -> NaN -> clamp gives 1
-                store_pixel(out, p, acc, spp);
+                if (team_leader) store_pixel(out, p, acc, spp);
                 phase = FETCH;
             }
             continue;
@@ -1011,7 +1051,7 @@ __global__ void RT_RENDER_BOUNDS render_kernel(DevScene S, FrameParams F, float*
             acc = rtm_add(acc, so);
             ++s;
             if (s >= spp) {
-                store_pixel(out, p, acc, spp);
+                if (team_leader) store_pixel(out, p, acc, spp);
                 phase = FETCH;
             } else {
                 Ro = C.position; Rd = cd; tri = tc; k = kc; j = 0;
@@ -1021,7 +1061,9 @@ __global__ void RT_RENDER_BOUNDS render_kernel(DevScene S, FrameParams F, float*
         }
     }
     if (COUNT) {
-        unsigned long long v[NCOUNTS] = {c.nodes, c.tris, c.rays, c.env, c.dropped, c.wave_trav, c.wave_outer};
+        if (!team_leader) c.env = 0;   // a team's lanes repeat its pixel's shading: counted once
+        unsigned long long v[NCOUNTS] = {c.nodes, c.tris, c.rays, c.env, c.dropped, c.wave_trav, c.wave_outer,
+                                          c.cyc_shade, c.cyc_trav};
 #pragma unroll
         for (int q = 0; q < NCOUNTS; ++q) {
             unsigned long long x = v[q];
@@ -1121,7 +1163,7 @@ __global__ void RT_RESUME_BOUNDS render_resume_kernel(DevScene S, FrameParams F,
                                                       const LaunchConst* __restrict__ lconst) {
     extern __shared__ int lds_stack[];
     const int B = blockDim.x;
-    Cnt c{0, 0, 0, 0, 0, 0, 0};
+    Cnt c{0, 0, 0, 0, 0, 0, 0, 0, 0};
     const LaunchConst& C = *lconst;
     const float4* nodes = S.nodes;
     const float4* tris = S.tri_geo;
@@ -1184,6 +1226,7 @@ __global__ void RT_RESUME_BOUNDS render_resume_kernel(DevScene S, FrameParams F,
     };
 
     while (true) {
+        const unsigned long long t_iter = COUNT ? clock64() : 0;
         // -- refill: ballot the lanes that need a pixel, one atomic per wave --
         const unsigned long long need = __ballot(phase == FETCH);
         if (need) {
@@ -1319,14 +1362,21 @@ __global__ void RT_RESUME_BOUNDS render_resume_kernel(DevScene S, FrameParams F,
         }
 
         // -- traversal rounds until at least F.resume_min lanes have no ray in flight --
+        unsigned long long t_mid = 0;
+        if (COUNT) {
+            t_mid = clock64();
+            if (lane == 0) c.cyc_shade += t_mid - t_iter;
+        }
         while (true) {
             if (tracing && fast_round<COUNT, SMEM, OVF>(S, T, nb, tb, lst, kstride, c)) tracing = false;
             const unsigned long long tr = __ballot(tracing);
             if (tr == 0 || 64 - __popcll(tr) >= F.resume_min) break;
         }
+        if (COUNT && lane == 0) c.cyc_trav += clock64() - t_mid;
     }
     if (COUNT) {
-        unsigned long long v[NCOUNTS] = {c.nodes, c.tris, c.rays, c.env, c.dropped, c.wave_trav, c.wave_outer};
+        unsigned long long v[NCOUNTS] = {c.nodes, c.tris, c.rays, c.env, c.dropped, c.wave_trav, c.wave_outer,
+                                          c.cyc_shade, c.cyc_trav};
 #pragma unroll
         for (int q = 0; q < NCOUNTS; ++q) {
             unsigned long long x = v[q];
@@ -1354,11 +1404,10 @@ hipError_t launch_t(const DevScene& sc, const FrameParams& fp, int block, float*
     if (TRAV == TRAV_FAST && sc.nbrute > 0 && RT_BRUTE_COMPACT)
         lds = std::max(lds, (size_t)(block / 64) * BRUTE_WAVE_LDS);
     if (BRUTE)
-        lds = (size_t)(block / 64) * BRUTE_WAVE_LDS + (size_t)sc.nbrute * 48 + (size_t)sc.ntri * 64 +
+        lds = (size_t)(block / 64) * BRUTE_WAVE_LDS + (size_t)sc.nbrute * 64 + (size_t)sc.ntri * 64 +
               (size_t)sc.nmat * 24;
     if (SMEM) lds += (size_t)(kNodeF4 * sc.nnodes + 3 * sc.ntri) * sizeof(float4);
-    const int64_t need = (fp.nloc + block - 1) / block;
-    if (need <= 0) return hipSuccess;
+    if (fp.nloc <= 0) return hipSuccess;
     // persistent grid: as many blocks as the device keeps resident (pixels are handed out by d_work)
     int dev = 0, cus = 0, per_cu = 0;
     hipError_t e = hipGetDevice(&dev);
@@ -1368,19 +1417,32 @@ hipError_t launch_t(const DevScene& sc, const FrameParams& fp, int block, float*
     if (e == hipSuccess) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kfn, block, lds);
     if (e != hipSuccess) return e;
     const int64_t resident = (int64_t)std::max(1, cus) * std::max(1, per_cu);
+    // brute-force teams: a tile with fewer pixels than the device has lanes (a row slice of a
+    // multi-GPU frame) gives each pixel 2 or 4 lanes that split its box tests
+    FrameParams f = fp;
+    f.team = 1;
+    if (BRUTE) {
+        f.team = fp.team;
+        if (f.team == 0) {
+            const int64_t lanes = resident * block;
+            f.team = 1;
+            while (f.team < 4 && fp.nloc * (f.team * 2) <= lanes) f.team *= 2;
+        }
+    }
+    const int64_t need = (fp.nloc * f.team + block - 1) / block;
     const int64_t grid = std::min(need, resident);
     e = hipMemsetAsync(d_work, 0, sizeof(unsigned int), stream);
     if (e != hipSuccess) return e;
     // the per-launch constants live after the counter in the same scratch block
     LaunchConst* lc = reinterpret_cast<LaunchConst*>(reinterpret_cast<char*>(d_work) + 64);
-    hipLaunchKernelGGL(make_const_kernel, dim3(1), dim3(64), 0, stream, fp, lc);
+    hipLaunchKernelGGL(make_const_kernel, dim3(1), dim3(64), 0, stream, f, lc);
     if (RESUME)
         hipLaunchKernelGGL((render_resume_kernel<COUNT, LOG, SMEM, OVF>), dim3((unsigned)grid), dim3(block), lds, stream,
-                           sc, fp, d_out, d_counts, d_work, (const LaunchConst*)lc);
+                           sc, f, d_out, d_counts, d_work, (const LaunchConst*)lc);
     else
         hipLaunchKernelGGL((render_kernel<TRAV, COUNT, LOG, SMEM, OVF, BRUTE>), dim3((unsigned)grid), dim3(block), lds,
                            stream,
-                           sc, fp, d_out, d_counts, d_work, (const LaunchConst*)lc);
+                           sc, f, d_out, d_counts, d_work, (const LaunchConst*)lc);
     return hipGetLastError();
 }
 
@@ -1411,7 +1473,7 @@ __global__ void __launch_bounds__(256) debug_trace_kernel(DevScene S, const floa
     extern __shared__ int lds_stack[];
     const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= n) return;
-    Cnt c{0, 0, 0, 0, 0, 0, 0};
+    Cnt c{0, 0, 0, 0, 0, 0, 0, 0, 0};
     const float* r = rays + 6 * t;
     const Hit h = trace<TRAV, false>(S, S.nodes, S.tri_geo, rtm_v3(r[3], r[4], r[5]), rtm_v3(r[0], r[1], r[2]),
                                      lds_stack + threadIdx.x, blockDim.x, lane_stack(S, lds_stack), c);
@@ -1477,7 +1539,10 @@ hipError_t launch_fast(const DevScene& sc, const FrameParams& fp, int block, flo
                                                                           stream);
         return launch_t<TRAV_FAST, COUNT, false, false, true>(sc, fp, block, d_out, d_counts, d_work, stream);
     }
-    if (sc.ntri > 0 && sc.nbrute > 0 && RT_BRUTE_COMPACT && RT_BRUTE_LDS && sc.ntri <= 1024)
+    // BRUTE stages the scene in LDS: only while two blocks still fit a CU
+    const size_t brute_lds = (size_t)(block / 64) * BRUTE_WAVE_LDS + (size_t)sc.nbrute * 64 +
+                             (size_t)sc.ntri * 64 + (size_t)sc.nmat * 24;
+    if (sc.ntri > 0 && sc.nbrute > 0 && RT_BRUTE_COMPACT && RT_BRUTE_LDS && brute_lds <= 80 * 1024)
         return launch_t<TRAV_FAST, COUNT, false, false, false, false, true>(sc, fp, block, d_out, d_counts, d_work,
                                                                             stream);
     if (smem) return launch_t<TRAV_FAST, COUNT, false, true>(sc, fp, block, d_out, d_counts, d_work, stream);

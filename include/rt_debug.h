@@ -31,9 +31,10 @@ int rt_debug_pixel_log(rt_ctx* ctx, int traversal, const float cam[10], const fl
  * ones: out[5] = traversal-loop iterations issued by waves (an iteration
  * counts once per wave however many lanes take part), out[6] = render-loop
  * iterations of all waves.  out[0] + out[1] over 64 * out[5] is the SIMD
- * efficiency of the traversal loop. */
+ * efficiency of the traversal loop.  Resumable tree walk only: out[7] / out[8] =
+ * clock cycles the waves spent outside / inside the traversal rounds. */
 int rt_debug_wave_counts(rt_ctx* ctx, const float cam[10], const float env[5], int64_t npix, int spp,
-                         int max_bounce, uint64_t out[7]);
+                         int max_bounce, uint64_t out[9]);
 
 /* Scene facts: out[0] = FAST layout available (1/0), out[1] = FAST stack
  * depth, out[2] = internal nodes, out[3] = triangles. */

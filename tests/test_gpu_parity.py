@@ -160,6 +160,36 @@ def test_brute_force_path_matches_tree_walk(kl, case):
     assert brute_counts["node_fetches"] == brute_counts["rays"] * (sc.faceData.size // 10)
 
 
+@pytest.mark.parametrize("case", ["cornell_64_s4", "cornell_64_b0"])
+def test_brute_force_teams_render_identically(kl, case):
+    """team = lanes sharing one pixel's box tests (auto for small tiles): the frame and the work
+    counts do not depend on it, whole frame or one row tile of a 3-way split."""
+    import torch
+    from ensem3a_openclraytracer_amd import distributed as D
+    sc, cam, env, npix, spp, mb, ibl = W.PARITY_CASES[case].inputs()
+    frames, counts = [], []
+    try:
+        for team in (1, 2, 4, 0):
+            kl.native.set_option("team", team)
+            frames.append(_launch(kl, sc, cam, env, npix, spp, mb, ibl, "fast"))
+            counts.append(kl.native.count_work(cam, env, npix, spp, mb))
+            w = int(cam[6])
+            t = torch.zeros(3 * w * D.max_tile_rows(npix, w, 3), dtype=torch.float32, device="cuda")
+            kl.native.render_device(cam, env, npix, spp, mb, 1, 3, t.data_ptr(),
+                                    torch.cuda.current_stream().cuda_stream)
+            torch.cuda.synchronize()
+            want = frames[-1].reshape(-1, 3 * w)[1::3].ravel()
+            np.testing.assert_array_equal(t.cpu().numpy()[:want.size], want)
+    finally:
+        kl.native.set_option("team", 0)
+    for f, c in zip(frames[1:], counts[1:]):
+        np.testing.assert_array_equal(f, frames[0])
+        assert (c["rays"], c["node_fetches"], c["env_lookups"]) == \
+            (counts[0]["rays"], counts[0]["node_fetches"], counts[0]["env_lookups"])
+    with pytest.raises(_native.NativeError, match="team"):
+        kl.native.set_option("team", 3)
+
+
 def test_brute_force_trace_kat(kl, kat_ref):
     sc = W.load_scene("cornell")
     ctx = kl.native

@@ -25,6 +25,7 @@ for name in sys.argv[1:] or ["C2"]:
                "per_sample": {k: round(v / samples, 3) for k, v in c.items()},
                "trav_simd_eff": round(lane_iters / max(1, 64 * c["wave_trav_iters"]), 4),
                "trav_iters_per_wave_render_iter": round(c["wave_trav_iters"] / max(1, c["wave_render_iters"]), 2),
-               "rays_per_lane_render_iter": round(c["rays"] / max(1, 64 * c["wave_render_iters"]), 4)}
+               "rays_per_lane_render_iter": round(c["rays"] / max(1, 64 * c["wave_render_iters"]), 4),
+               "trav_cycle_share": round(c["cycles_trav"] / max(1, c["cycles_trav"] + c["cycles_shade"]), 4)}
         print(json.dumps(out), flush=True)
         ctx.close()
