@@ -132,6 +132,28 @@ class KernelLauncher(object):
         out = h_img_out.reshape(-1)
         self._ctx.render(cam[:10], env[:5], imgDim, int(spp), int(maxBounce), out=out)
 
+    def launch_Raytracing_rgb8(self, h_img_out, h_vertex_p, h_vertex_n, h_vertex_uv, h_face_data,
+                               h_material_data, h_light_data, h_BVH, h_cam, h_envData, imgDim, spp, maxBounce,
+                               h_IBL, gamma: bool = False):
+        """``launch_Raytracing`` fused with the output stage: ``h_img_out`` is uint8 ``[3*imgDim]`` and
+        receives ``(frame*255).astype('uint8')`` (FileManager.saveImg, FileManager.py:334-336),
+        after the ImgProcessing gamma when ``gamma`` -- quantized on the device, so a quarter of
+        the bytes cross PCIe."""
+        if not isinstance(h_img_out, np.ndarray) or h_img_out.dtype != np.uint8 or \
+                not h_img_out.flags.c_contiguous:
+            raise TypeError("h_img_out must be a C-contiguous uint8 numpy array")
+        imgDim = int(imgDim)
+        if h_img_out.size < 3 * imgDim:
+            raise ValueError(f"h_img_out has {h_img_out.size} bytes, needs 3*imgDim = {3 * imgDim}")
+        cam = _native.f32(h_cam).reshape(-1)
+        env = _native.f32(h_envData).reshape(-1)
+        if cam.size < 10 or env.size < 5:
+            raise ValueError("h_cam needs 10 floats and h_envData 5")
+        self._upload_scene(h_vertex_p, h_vertex_n, h_vertex_uv, h_face_data, h_material_data, h_BVH)
+        self._upload_env(h_IBL)
+        self._ctx.render_rgb8(cam[:10], env[:5], imgDim, int(spp), int(maxBounce), gamma=gamma,
+                              out=h_img_out.reshape(-1))
+
     def launch_ImgProcessing(self, h_src, h_out, SIZE):
         """Gamma 2.2 of ``ImgProcessing.cl``: ``h_out[k] = min(h_src[k], 1) ** 2.2`` for ``k < 3*SIZE*SIZE``."""
         src = _native.f32(h_src).reshape(-1)

@@ -25,6 +25,7 @@ RT_BVH_SAH = 1
 EXPORTED = (
     "rt_create", "rt_destroy", "rt_last_error", "rt_set_scene", "rt_set_env", "rt_set_option",
     "rt_render", "rt_render_device", "rt_tile_rows", "rt_count_work", "rt_work_bytes", "rt_gamma",
+    "rt_render_rgb8", "rt_rgb8_device", "rt_rgb8",
     "rt_bvh_build", "rt_device_count", "rt_debug_math", "rt_debug_trace", "rt_debug_scene_info", "rt_debug_pixel_log",
     "rt_debug_wave_counts",
     "rt_obj_parse", "rt_obj_size", "rt_obj_copy", "rt_obj_free", "rt_obj_last_error",
@@ -77,6 +78,9 @@ def lib():
             "rt_count_work": (_i32, [_c_p, _c_p, _c_p, _i64, _i32, _i32, _i32, _i32, _c_p]),
             "rt_work_bytes": (_i32, [_c_p, _c_p]),
             "rt_gamma": (_i32, [_c_p, _c_p, _c_p, _i64]),
+            "rt_render_rgb8": (_i32, [_c_p, _c_p, _c_p, _i64, _i32, _i32, _i32, _c_p]),
+            "rt_rgb8_device": (_i32, [_c_p, _i32, _c_p, _c_p, _i64, _i32, _c_p]),
+            "rt_rgb8": (_i32, [_c_p, _c_p, _c_p, _i64, _i32]),
             "rt_bvh_build": (_i32, [_c_p, _i64, _c_p, _i64, _c_p, ctypes.POINTER(_i64)]),
             "rt_device_count": (_i32, []),
             "rt_obj_parse": (_i32, [_c_p, _i64, ctypes.POINTER(_c_p)]),
@@ -205,6 +209,33 @@ class Context:
             out = np.zeros_like(s)
         self._check(lib().rt_gamma(self.handle, ptr(s), out.ctypes.data, s.size))
         return out
+
+    def render_rgb8(self, cam, env, npix: int, spp: int, max_bounce: int, gamma: bool = False,
+                    out: np.ndarray = None) -> np.ndarray:
+        """Render and quantize on the device: uint8[3*npix] = (frame*255).astype(uint8) (gamma first if asked)."""
+        c, e = f32(cam), f32(env)
+        if c.size != 10 or e.size != 5:
+            raise ValueError("cam must have 10 floats and envData 5")
+        if out is None:
+            out = np.zeros(3 * int(npix), dtype=np.uint8)
+        if out.dtype != np.uint8 or not out.flags.c_contiguous or out.size < 3 * int(npix):
+            raise ValueError("output must be a contiguous uint8 array of 3*imgDim elements")
+        self._check(lib().rt_render_rgb8(self.handle, ptr(c), ptr(e), int(npix), int(spp), int(max_bounce),
+                                         int(bool(gamma)), out.ctypes.data))
+        return out
+
+    def rgb8(self, src, gamma: bool = False, out=None) -> np.ndarray:
+        """Host float32 -> uint8 through the device output stage."""
+        s = f32(src).reshape(-1)
+        if out is None:
+            out = np.zeros(s.size, dtype=np.uint8)
+        self._check(lib().rt_rgb8(self.handle, ptr(s), out.ctypes.data, s.size, int(bool(gamma))))
+        return out
+
+    def rgb8_device(self, d_in_ptr: int, d_out_ptr: int, n: int, gamma: bool = False, stream_ptr: int = 0,
+                    device_index: int = 0) -> None:
+        self._check(lib().rt_rgb8_device(self.handle, int(device_index), _c_p(int(d_in_ptr)), _c_p(int(d_out_ptr)),
+                                         int(n), int(bool(gamma)), _c_p(int(stream_ptr)) if stream_ptr else None))
 
     def debug_math(self, fn: int, x, y=None):
         x = f32(x)

@@ -44,8 +44,8 @@ struct Device {
     hipStream_t stream = nullptr;
     int cus = 0;                  // compute units (sizes the FAST stack overflow buffer)
     DevBuf stack_ovf;             // FAST traversal stack entries beyond the LDS part
-    DevBuf nodes, brute, bvh9, tri_geo, tri_shade, tri_frame, mat, ibl, out, counts, work, scratch_a, scratch_b;
-    float* host_stage = nullptr;  // pinned staging for rt_render
+    DevBuf nodes, brute, bvh9, tri_geo, tri_shade, tri_frame, mat, ibl, out, out8, counts, work, scratch_a, scratch_b;
+    char* host_stage = nullptr;   // pinned staging for rt_render / rt_render_rgb8
     size_t host_stage_bytes = 0;
 };
 
@@ -678,15 +678,20 @@ int rt_render_device(rt_ctx* ctx, int device_index, const float cam[10], const f
     return RT_OK;
 }
 
-int rt_render(rt_ctx* ctx, const float cam[10], const float env[5], int64_t npix, int spp, int max_bounce,
-              float* out_rgb) {
+namespace {
+// rt_render / rt_render_rgb8: every device renders its rows (row r on device r mod n), then, for
+// rgb8 >= 0, quantizes them on the device (rgb8 = 1: gamma first) so 1 byte per channel crosses
+// PCIe; the host de-interleaves the rows into out (elem = 4 or 1 bytes per channel).
+int render_host(rt_ctx* ctx, const float cam[10], const float env[5], int64_t npix, int spp, int max_bounce,
+                void* out, int rgb8) {
     rt::FrameParams fp0;
     int st = check_frame(ctx, cam, env, npix, spp, 0, 1, &fp0);
     if (st) return st;
-    if (!out_rgb) return set_err(ctx, RT_ERR_ARG, "out_rgb must not be NULL");
+    if (!out) return set_err(ctx, RT_ERR_ARG, "output must not be NULL");
     if (max_bounce > 4096) return set_err(ctx, RT_ERR_ARG, "maxBounce %d > 4096", max_bounce);
     const int nd = (int)ctx->devs.size();
     const int W = fp0.width;
+    const size_t elem = rgb8 >= 0 ? 1 : sizeof(float);
     // Launch every device, then read back: devices run concurrently.
     for (int k = 0; k < nd; ++k) {
         Device& d = ctx->devs[k];
@@ -696,9 +701,9 @@ int rt_render(rt_ctx* ctx, const float cam[10], const float env[5], int64_t npix
         fp.max_bounce = max_bounce;
         fp.nloc = rt_tile_rows(npix, W, k, nd) * W;
         HIP_OR_RET(ctx, hipSetDevice(d.id));
-        const size_t bytes = (size_t)fp.nloc * 3 * sizeof(float);
+        const size_t bytes = (size_t)fp.nloc * 3 * elem;
         if (bytes == 0) continue;
-        HIP_OR_RET(ctx, ensure(d.out, bytes));
+        HIP_OR_RET(ctx, ensure(d.out, (size_t)fp.nloc * 3 * sizeof(float)));
         if (d.host_stage_bytes < bytes) {
             if (d.host_stage) HIP_OR_RET(ctx, hipHostFree(d.host_stage));
             d.host_stage = nullptr;
@@ -708,24 +713,74 @@ int rt_render(rt_ctx* ctx, const float cam[10], const float env[5], int64_t npix
         }
         HIP_OR_RET(ctx, rt::launch_render(dev_scene(ctx, d), fp, effective_traversal(ctx), ctx->block,
                                           (float*)d.out.p, nullptr, (unsigned int*)d.work.p, d.stream));
-        HIP_OR_RET(ctx, hipMemcpyAsync(d.host_stage, d.out.p, bytes, hipMemcpyDeviceToHost, d.stream));
+        const void* src = d.out.p;
+        if (rgb8 >= 0) {
+            HIP_OR_RET(ctx, ensure(d.out8, bytes));
+            HIP_OR_RET(ctx, rt::launch_rgb8((const float*)d.out.p, (uint8_t*)d.out8.p, (int64_t)fp.nloc * 3,
+                                            rgb8 == 1, d.stream));
+            src = d.out8.p;
+        }
+        HIP_OR_RET(ctx, hipMemcpyAsync(d.host_stage, src, bytes, hipMemcpyDeviceToHost, d.stream));
     }
+    char* dst = static_cast<char*>(out);
     for (int k = 0; k < nd; ++k) {
         Device& d = ctx->devs[k];
         HIP_OR_RET(ctx, hipSetDevice(d.id));
         HIP_OR_RET(ctx, hipStreamSynchronize(d.stream));
         const int64_t rows = rt_tile_rows(npix, W, k, nd);
         if (nd == 1) {
-            std::memcpy(out_rgb, d.host_stage, (size_t)npix * 3 * sizeof(float));
+            std::memcpy(dst, d.host_stage, (size_t)npix * 3 * elem);
             continue;
         }
         for (int64_t r = 0; r < rows; ++r) {
             const int64_t gr = (int64_t)k + r * nd;
             const int64_t first = gr * W;
             const int64_t count = std::min<int64_t>(W, npix - first);
-            std::memcpy(out_rgb + 3 * first, d.host_stage + 3 * r * W, (size_t)count * 3 * sizeof(float));
+            std::memcpy(dst + 3 * first * elem, d.host_stage + 3 * r * W * elem, (size_t)count * 3 * elem);
         }
     }
+    return RT_OK;
+}
+}  // namespace
+
+int rt_render(rt_ctx* ctx, const float cam[10], const float env[5], int64_t npix, int spp, int max_bounce,
+              float* out_rgb) {
+    return render_host(ctx, cam, env, npix, spp, max_bounce, out_rgb, -1);
+}
+
+int rt_render_rgb8(rt_ctx* ctx, const float cam[10], const float env[5], int64_t npix, int spp, int max_bounce,
+                   int gamma, uint8_t* out_rgb8) {
+    if (ctx && gamma != 0 && gamma != 1) return set_err(ctx, RT_ERR_ARG, "gamma must be 0 or 1");
+    return render_host(ctx, cam, env, npix, spp, max_bounce, out_rgb8, gamma);
+}
+
+int rt_rgb8_device(rt_ctx* ctx, int device_index, const float* d_in, uint8_t* d_out, int64_t n, int gamma,
+                   void* stream) {
+    if (!ctx) return set_err(nullptr, RT_ERR_ARG, "null context");
+    if (device_index < 0 || device_index >= (int)ctx->devs.size())
+        return set_err(ctx, RT_ERR_ARG, "device_index %d out of range", device_index);
+    if (n < 0 || (n > 0 && (!d_in || !d_out)) || (gamma != 0 && gamma != 1))
+        return set_err(ctx, RT_ERR_ARG, "bad arguments");
+    if (((uintptr_t)d_in & 15) || ((uintptr_t)d_out & 3))
+        return set_err(ctx, RT_ERR_ARG, "d_in must be 16-byte and d_out 4-byte aligned");
+    HIP_OR_RET(ctx, hipSetDevice(ctx->devs[device_index].id));
+    HIP_OR_RET(ctx, rt::launch_rgb8(d_in, d_out, n, gamma == 1, (hipStream_t)stream));
+    return RT_OK;
+}
+
+int rt_rgb8(rt_ctx* ctx, const float* in, uint8_t* out, int64_t n, int gamma) {
+    if (!ctx) return set_err(nullptr, RT_ERR_ARG, "null context");
+    if (n < 0 || (n > 0 && (!in || !out)) || (gamma != 0 && gamma != 1))
+        return set_err(ctx, RT_ERR_ARG, "bad arguments");
+    if (n == 0) return RT_OK;
+    Device& d = ctx->devs[0];
+    HIP_OR_RET(ctx, hipSetDevice(d.id));
+    HIP_OR_RET(ctx, ensure(d.scratch_a, (size_t)n * sizeof(float)));
+    HIP_OR_RET(ctx, ensure(d.scratch_b, (size_t)n));
+    HIP_OR_RET(ctx, hipMemcpyAsync(d.scratch_a.p, in, (size_t)n * sizeof(float), hipMemcpyHostToDevice, d.stream));
+    HIP_OR_RET(ctx, rt::launch_rgb8((const float*)d.scratch_a.p, (uint8_t*)d.scratch_b.p, n, gamma == 1, d.stream));
+    HIP_OR_RET(ctx, hipMemcpyAsync(out, d.scratch_b.p, (size_t)n, hipMemcpyDeviceToHost, d.stream));
+    HIP_OR_RET(ctx, hipStreamSynchronize(d.stream));
     return RT_OK;
 }
 

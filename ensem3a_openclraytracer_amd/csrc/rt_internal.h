@@ -82,6 +82,7 @@ hipError_t launch_render(const DevScene& sc, const FrameParams& fp, int traversa
                          float* d_out, unsigned long long* d_counts, unsigned int* d_work, hipStream_t stream);
 hipError_t launch_prep_frames(const DevScene& sc, float4* frame, hipStream_t stream);
 hipError_t launch_gamma(const float* d_in, float* d_out, int64_t n, hipStream_t stream);
+hipError_t launch_rgb8(const float* d_in, uint8_t* d_out, int64_t n, bool gamma, hipStream_t stream);
 // test hooks
 hipError_t launch_debug_math(int fn, const float* x, const float* y, float* out, int64_t n, hipStream_t stream);
 hipError_t launch_debug_log(const DevScene& sc, const FrameParams& fp, int traversal, float* d_out,

@@ -454,11 +454,11 @@ __device__ __forceinline__ void wave_lds_sync() {
     __builtin_amdgcn_wave_barrier();
 }
 
-template <bool COUNT>
-// Teams (ts = 2 or 4 lanes per pixel, when a tile has fewer pixels than the GPU has lanes): the
-// ts lanes of a team carry the same path (identical arithmetic), split the box tests between
+// Teams (ts = 2, 4 or 8 lanes per pixel, when a tile has fewer pixels than the GPU has lanes):
+// the ts lanes of a team carry the same path (identical arithmetic), split the box tests between
 // them (lane `sub` of the team tests records sub, sub + ts, ...; records read from the LDS copy
 // at boxrec, 1 float4 per triangle, and mtrec) and share one owner slot (the team's first lane).
+template <bool COUNT>
 __device__ Hit trace_brute_compact(const DevScene& S, rtm_f3 o, rtm_f3 d, char* wl, const float4* mtrec,
                                    unsigned mtstride, Cnt& c, int ts = 1, const float4* boxrec = nullptr) {
     const unsigned lane = threadIdx.x & 63;
@@ -823,7 +823,7 @@ enum Phase { FETCH = 0, PRIMARY = 1, PREP = 2, BOUNCE = 3, SUN = 4, DONE = 5 };
 // base + (its rank among the requesting lanes) -- so no lane idles while the
 // rest of its wave finishes a slower pixel.  Per loop iteration every busy
 // lane traces exactly one ray (primary, bounce or sun ray).
-template <int TRAV, bool COUNT, bool LOG = false, bool SMEM = false, bool OVF = false, bool BRUTE = false>
+template <int TRAV, bool COUNT, bool LOG = false, bool SMEM = false, bool OVF = false, int BRUTE = 0>
 __global__ void RT_RENDER_BOUNDS render_kernel(DevScene S, FrameParams F, float* __restrict__ out,
                                                unsigned long long* __restrict__ counts,
                                                unsigned int* __restrict__ work_counter,
@@ -843,8 +843,10 @@ __global__ void RT_RENDER_BOUNDS render_kernel(DevScene S, FrameParams F, float*
     if (BRUTE) {
         float4* lr = reinterpret_cast<float4*>(reinterpret_cast<char*>(lds_stack) + (B / 64) * BRUTE_WAVE_LDS);
         float4* lb = lr + 3 * S.nbrute;                  // lo.xyz hi.x of each record (team box tests)
-        for (int q = threadIdx.x; q < S.nbrute; q += B) lb[q] = S.brute[4 * q];
-        boxrec = lb;
+        if (BRUTE == 2) {
+            for (int q = threadIdx.x; q < S.nbrute; q += B) lb[q] = S.brute[4 * q];
+            boxrec = lb;
+        }
         float4* ls = lb + S.nbrute;
         float4* lf = ls + S.ntri;
         float* lm = reinterpret_cast<float*>(lf + 3 * S.ntri);
@@ -879,7 +881,7 @@ __global__ void RT_RENDER_BOUNDS render_kernel(DevScene S, FrameParams F, float*
     const int spp = F.spp, maxB = F.max_bounce;
     const unsigned int nloc = (unsigned int)F.nloc;
     const int lane = threadIdx.x & 63;
-    const int ts = BRUTE ? F.team : 1;                           // lanes per pixel (1, 2, 4, 8)
+    const int ts = BRUTE == 2 ? F.team : 1;                      // lanes per pixel (1, 2, 4, 8)
     const int team_lane0 = lane & ~(ts - 1);
     const bool team_leader = lane == team_lane0;
     const unsigned long long team_leaders = ts == 1 ? ~0ull : ts == 2 ? 0x5555555555555555ull
@@ -997,7 +999,7 @@ __global__ void RT_RENDER_BOUNDS render_kernel(DevScene S, FrameParams F, float*
         // -- one ray per busy lane --
         const rtm_f3 to = (phase == PRIMARY) ? C.position : Bo;
         const rtm_f3 td = (phase == PRIMARY) ? cd : ((phase == BOUNCE) ? Bd : C.sun);
-        const Hit h = trace<TRAV, COUNT, SMEM, OVF, BRUTE>(S, nodes, tris, to, td, stk, B, lst, c, mtrec, ts, boxrec);
+        const Hit h = trace<TRAV, COUNT, SMEM, OVF, BRUTE != 0>(S, nodes, tris, to, td, stk, B, lst, c, mtrec, ts, boxrec);
         bool finish = false;
         if (phase == PRIMARY) {
             tc = h.tri;
@@ -1394,6 +1396,32 @@ __global__ void gamma_kernel(const float* __restrict__ in, float* __restrict__ o
     }
 }
 
+// Output stage (FileManager.py:334-336 saveImg: (data*255).astype('uint8'); with gamma first the
+// ImgProcessing.cl:1-10 kernel, as gamma_kernel above).  Four elements per thread: float4 in,
+// one 32-bit word of bytes out.  v*255 rounds in fp32 like numpy's float32 product; the
+// conversion truncates toward zero like numpy's cast for every v*255 in [0, 256) (rendered
+// frames are clamped to [0, 1]); outside that range it saturates (NaN -> 0).
+template <bool GAMMA>
+__device__ __forceinline__ unsigned rgb8_byte(float v) {
+    if (GAMMA) v = powf(fminf(v, 1.0f), 2.2f);
+    const float x = v * 255.0f;
+    return (unsigned)min(max((int)x, 0), 255);   // v_cvt_i32_f32 truncates, NaN -> 0
+}
+
+template <bool GAMMA>
+__global__ void rgb8_kernel(const float* __restrict__ in, uint8_t* __restrict__ out, int64_t n) {
+    const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;   // group of 4 elements
+    const int64_t i = 4 * q;
+    if (i + 4 <= n) {
+        const float4 v = *reinterpret_cast<const float4*>(in + i);
+        const unsigned w = rgb8_byte<GAMMA>(v.x) | (rgb8_byte<GAMMA>(v.y) << 8) | (rgb8_byte<GAMMA>(v.z) << 16) |
+                           (rgb8_byte<GAMMA>(v.w) << 24);
+        *reinterpret_cast<unsigned*>(out + i) = w;
+    } else {
+        for (int64_t k = i; k < n; ++k) out[k] = (uint8_t)rgb8_byte<GAMMA>(in[k]);
+    }
+}
+
 template <int TRAV, bool COUNT, bool LOG, bool SMEM = false, bool RESUME = false, bool OVF = false,
           bool BRUTE = false>
 hipError_t launch_t(const DevScene& sc, const FrameParams& fp, int block, float* d_out, unsigned long long* d_counts,
@@ -1413,7 +1441,7 @@ hipError_t launch_t(const DevScene& sc, const FrameParams& fp, int block, float*
     hipError_t e = hipGetDevice(&dev);
     if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     const void* kfn = RESUME ? (const void*)render_resume_kernel<COUNT, LOG, SMEM, OVF>
-                             : (const void*)render_kernel<TRAV, COUNT, LOG, SMEM, OVF, BRUTE>;
+                             : (const void*)render_kernel<TRAV, COUNT, LOG, SMEM, OVF, BRUTE ? 1 : 0>;
     if (e == hipSuccess) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kfn, block, lds);
     if (e != hipSuccess) return e;
     const int64_t resident = (int64_t)std::max(1, cus) * std::max(1, per_cu);
@@ -1430,7 +1458,15 @@ hipError_t launch_t(const DevScene& sc, const FrameParams& fp, int block, float*
         }
     }
     const int64_t need = (fp.nloc * f.team + block - 1) / block;
-    const int64_t grid = std::min(need, resident);
+    int64_t grid = std::min(need, resident);
+    // teams run their own instantiation (the ts = 1 kernel keeps the scalar box loop)
+    const void* tfn = (const void*)render_kernel<TRAV, COUNT, LOG, SMEM, OVF, BRUTE ? 2 : 0>;
+    if (BRUTE && f.team > 1) {
+        int per_cu_t = 0;
+        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu_t, tfn, block, lds);
+        if (e != hipSuccess) return e;
+        grid = std::min(need, (int64_t)std::max(1, cus) * std::max(1, per_cu_t));
+    }
     e = hipMemsetAsync(d_work, 0, sizeof(unsigned int), stream);
     if (e != hipSuccess) return e;
     // the per-launch constants live after the counter in the same scratch block
@@ -1439,10 +1475,12 @@ hipError_t launch_t(const DevScene& sc, const FrameParams& fp, int block, float*
     if (RESUME)
         hipLaunchKernelGGL((render_resume_kernel<COUNT, LOG, SMEM, OVF>), dim3((unsigned)grid), dim3(block), lds, stream,
                            sc, f, d_out, d_counts, d_work, (const LaunchConst*)lc);
+    else if (BRUTE && f.team > 1)
+        hipLaunchKernelGGL((render_kernel<TRAV, COUNT, LOG, SMEM, OVF, BRUTE ? 2 : 0>), dim3((unsigned)grid),
+                           dim3(block), lds, stream, sc, f, d_out, d_counts, d_work, (const LaunchConst*)lc);
     else
-        hipLaunchKernelGGL((render_kernel<TRAV, COUNT, LOG, SMEM, OVF, BRUTE>), dim3((unsigned)grid), dim3(block), lds,
-                           stream,
-                           sc, f, d_out, d_counts, d_work, (const LaunchConst*)lc);
+        hipLaunchKernelGGL((render_kernel<TRAV, COUNT, LOG, SMEM, OVF, BRUTE ? 1 : 0>), dim3((unsigned)grid),
+                           dim3(block), lds, stream, sc, f, d_out, d_counts, d_work, (const LaunchConst*)lc);
     return hipGetLastError();
 }
 
@@ -1559,6 +1597,19 @@ hipError_t launch_render(const DevScene& sc, const FrameParams& fp, int traversa
     }
     return d_counts ? launch_fast<true>(sc, fp, block, d_out, d_counts, d_work, stream)
                     : launch_fast<false>(sc, fp, block, d_out, d_counts, d_work, stream);
+}
+
+hipError_t launch_rgb8(const float* d_in, uint8_t* d_out, int64_t n, bool gamma, hipStream_t stream) {
+    if (n <= 0) return hipSuccess;
+    // float4 loads and 32-bit stores need 16- and 4-byte alignment (torch / hipMalloc buffers have it)
+    if (((uintptr_t)d_in & 15) || ((uintptr_t)d_out & 3)) return hipErrorInvalidValue;
+    const int block = 256;
+    const int64_t grid = ((n + 3) / 4 + block - 1) / block;
+    if (gamma)
+        hipLaunchKernelGGL(rgb8_kernel<true>, dim3((unsigned)grid), dim3(block), 0, stream, d_in, d_out, n);
+    else
+        hipLaunchKernelGGL(rgb8_kernel<false>, dim3((unsigned)grid), dim3(block), 0, stream, d_in, d_out, n);
+    return hipGetLastError();
 }
 
 hipError_t launch_gamma(const float* d_in, float* d_out, int64_t n, hipStream_t stream) {

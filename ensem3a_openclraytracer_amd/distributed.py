@@ -61,17 +61,22 @@ def assemble(tiles, width: int, npix: int, world: int, out=None):
 
 
 def render_distributed(render_tile: Callable, npix: int, width: int, rank: int, world: int, device=None,
-                       group=None, gather: bool = True):
+                       group=None, gather: bool = True, quantize: Optional[Callable] = None):
     """Render this rank's rows with ``render_tile(row0, row_step, out_tile)`` and gather on rank 0.
 
     ``out_tile`` is a zero-initialised float32 tensor of ``3*width*max_rows``
     elements on ``device`` (the tail beyond this rank's rows stays zero).
     Returns the full frame (a flat tensor of ``3*npix``) on rank 0, the
     local tile on the other ranks.
+
+    ``quantize(tile) -> uint8 tile`` (the output stage, e.g. ``gpu_rgb8``) runs on every rank
+    before the gather, so the collective moves 1 byte per channel instead of 4.
     """
     mrows = max_tile_rows(npix, width, world)
     tile = torch.zeros(3 * width * mrows, dtype=torch.float32, device=device)
     render_tile(rank, world, tile)
+    if quantize is not None:
+        tile = quantize(tile)
     if world == 1:
         return tile[: 3 * npix]
     if not gather:
@@ -92,3 +97,14 @@ def gpu_tile_renderer(ctx, cam, env, npix: int, spp: int, max_bounce: int, devic
         ctx.render_device(cam, env, npix, spp, max_bounce, row0, row_step, out_tile.data_ptr(), s,
                           device_index=device_index)
     return render_tile
+
+
+def gpu_rgb8(ctx, gamma: bool = False, device_index: int = 0, stream: Optional[int] = None):
+    """``quantize`` for ``render_distributed``: the device output stage (``rt_rgb8_device``,
+    FileManager.saveImg's ``(data*255).astype('uint8')``, gamma first if asked)."""
+    def quantize(tile):
+        out = torch.empty(tile.numel(), dtype=torch.uint8, device=tile.device)
+        s = stream if stream is not None else torch.cuda.current_stream().cuda_stream
+        ctx.rgb8_device(tile.data_ptr(), out.data_ptr(), tile.numel(), gamma, s, device_index=device_index)
+        return out
+    return quantize

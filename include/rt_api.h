@@ -123,6 +123,26 @@ int rt_work_bytes(rt_ctx* ctx, double out[4]);
  * for k < n, blocking, host memory. */
 int rt_gamma(rt_ctx* ctx, const float* in, float* out, int64_t n);
 
+/* Output stage (8-bit frame), replacing FileManager.saveImg's quantization
+ * (FileManager.py:334-336: (data*255).astype('uint8')) and, with gamma = 1,
+ * the ImgProcessing.cl gamma applied first (KernelLauncher.launch_ImgProcessing,
+ * KernelLauncher.py:90-103): out[k] = (uint8)(v * 255) with v = in[k] or
+ * powr(min(in[k],1), 2.2).  Exact truncation for v*255 in [0, 256) -- every
+ * rendered value, the frame being clamped to [0,1]; saturating outside it
+ * (NaN -> 0).
+ *   rt_render_rgb8: rt_render, then quantize on the device(s); 3*npix bytes
+ *                   (row-major RGB) into caller-owned host memory, blocking.
+ *   rt_rgb8_device: quantize device memory d_in[n] -> d_out[n] on device
+ *                   device_index, enqueued on `stream` (the gather of the
+ *                   multi-process path moves these bytes); d_in 16-byte and
+ *                   d_out 4-byte aligned.
+ *   rt_rgb8:        host memory in -> out, blocking (device 0). */
+int rt_render_rgb8(rt_ctx* ctx, const float cam[10], const float env[5], int64_t npix, int spp,
+                   int max_bounce, int gamma, uint8_t* out_rgb8);
+int rt_rgb8_device(rt_ctx* ctx, int device_index, const float* d_in, uint8_t* d_out, int64_t n,
+                   int gamma, void* stream);
+int rt_rgb8(rt_ctx* ctx, const float* in, uint8_t* out, int64_t n, int gamma);
+
 /* BVH.py export built natively (bit-identical, see bvh_build.cpp):
  * out must hold 9*(2T-1) floats, T = nface/10; *out_nodes = nodes written. */
 int rt_bvh_build(const int32_t* face, int64_t nface, const float* vp, int64_t nvp,

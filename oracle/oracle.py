@@ -187,6 +187,23 @@ def math(fn: str, x, y=None):
     return out
 
 
+def gamma(x):
+    """ImgProcessing.cl:1-10 (powr(min(x,1), 2.2)), evaluated in float64 and rounded to float32;
+    powr is implementation-defined, so comparisons against it carry a tolerance."""
+    x = np.asarray(x, dtype=np.float32)
+    return np.power(np.minimum(x, np.float32(1)).astype(np.float64), 2.2).astype(np.float32)
+
+
+def rgb8(data, gamma_first: bool = False):
+    """Output stage of FileManager.saveImg (FileManager.py:334-336): ``(data*255).astype('uint8')``
+    on a float32 frame (the product is float32: numpy's weak Python-int promotion); optionally
+    after the gamma kernel (main.py:96-97 pairs them, commented out in the reference)."""
+    d = np.asarray(data, dtype=np.float32)
+    if gamma_first:
+        d = gamma(d)
+    return (d * 255).astype("uint8")
+
+
 def pixel_log(osc: OracleScene, cam, env, npix: int, spp: int, max_bounce: int, pixel: int, cap: int = 4096):
     cam, env = _f32(cam), _f32(env)
     log = np.zeros((cap, 16), np.float32)

@@ -43,7 +43,7 @@ def test_assemble_numpy_and_torch(npix, width, world):
     np.testing.assert_array_equal(got.numpy(), frame)
 
 
-def _worker(rank, world, port, case, q):
+def _worker(rank, world, port, case, q, quantize=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     wl = W.PARITY_CASES[case]
@@ -55,7 +55,8 @@ def _worker(rank, world, port, case, q):
         t = O.render(osc, cam, env, npix, spp, mb, row0=row0, row_step=row_step, nthreads=2)
         out_tile[: t.size] = torch.from_numpy(t)
 
-    frame = D.render_distributed(render_tile, npix, W_, rank, world)
+    qz = (lambda t: torch.from_numpy(O.rgb8(t.numpy()))) if quantize else None
+    frame = D.render_distributed(render_tile, npix, W_, rank, world, quantize=qz)
     if rank == 0:
         q.put(frame.numpy().copy())
     dist.destroy_process_group()
@@ -77,3 +78,23 @@ def test_gloo_tiled_render_is_bit_identical(case, world):
     sc, cam, env, npix, spp, mb, ibl = wl.inputs()
     full = O.render(O.OracleScene.from_scene(sc, ibl), cam, env, npix, spp, mb, nthreads=4)
     np.testing.assert_array_equal(frame, full)
+
+
+def test_gloo_quantized_gather_is_the_output_stage_of_the_full_frame():
+    """Tiles quantized to 8 bits before the gather (4x fewer bytes on the wire) assemble into
+    saveImg's (frame*255).astype(uint8) of the 1-rank frame."""
+    case, world = "cornell_64_s4", 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, case, q, True)) for r in range(world)]
+    for p in procs:
+        p.start()
+    frame = q.get(timeout=300)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    sc, cam, env, npix, spp, mb, ibl = W.PARITY_CASES[case].inputs()
+    full = O.render(O.OracleScene.from_scene(sc, ibl), cam, env, npix, spp, mb, nthreads=4)
+    assert frame.dtype == np.uint8
+    np.testing.assert_array_equal(frame, O.rgb8(full))

@@ -375,3 +375,61 @@ def test_reference_render_outpng(kl):
     mse = ((crop - z["crop"].astype(np.float64)) ** 2).mean()
     psnr = 10 * np.log10(255.0 ** 2 / mse)
     assert psnr >= 26.0, psnr
+
+
+def _rgb8_inputs():
+    rng = np.random.default_rng(17)
+    edges = np.array([k / 255 for k in range(256)], np.float32)
+    near = np.concatenate([np.nextafter(edges, np.float32(0)), np.nextafter(edges, np.float32(2))])
+    x = np.concatenate([rng.random(100_001, dtype=np.float32), edges, near, [0.0, 1.0, 0.5]]).astype(np.float32)
+    return np.clip(x, 0, 1).astype(np.float32)   # rendered frames are clamped to [0, 1]
+
+
+def test_rgb8_output_stage_bit_identical(kl):
+    """rt_rgb8 == FileManager.saveImg's (data*255).astype('uint8') on [0,1] (incl. every k/255 and its
+    float neighbours), odd lengths included (the vector kernel's tail)."""
+    x = _rgb8_inputs()
+    for n in (x.size, x.size - 1, 3, 1):
+        np.testing.assert_array_equal(kl.native.rgb8(x[:n]), O.rgb8(x[:n]))
+    # gamma first: bit-identical to quantizing the device's own gamma; within 1 of a float64 gamma
+    g = kl.native.rgb8(x, gamma=True)
+    np.testing.assert_array_equal(g, O.rgb8(kl.native.gamma(x)))
+    assert np.abs(g.astype(int) - O.rgb8(x, gamma_first=True).astype(int)).max() <= 1
+
+
+@pytest.mark.parametrize("case", ["cornell_64_s4", "serre_96x54_s4"])
+def test_render_rgb8_is_the_quantized_render(kl, case):
+    sc, cam, env, npix, spp, mb, ibl = W.PARITY_CASES[case].inputs()
+    f = _launch(kl, sc, cam, env, npix, spp, mb, ibl, "fast")
+    for gamma in (False, True):
+        out = np.zeros(3 * npix, np.uint8)
+        kl.launch_Raytracing_rgb8(out, sc.V_p, sc.V_n, sc.V_uv, sc.faceData, sc.materialData, sc.lightData,
+                                  sc.BVH.exportArray, cam, env, npix, spp, mb, ibl, gamma=gamma)
+        want = O.rgb8(kl.native.gamma(f)) if gamma else O.rgb8(f)
+        np.testing.assert_array_equal(out, want)
+
+
+def test_rgb8_device_quantized_tiles_assemble(kl):
+    """The multi-process path's fused output stage: per-tile rt_rgb8_device, uint8 assembly."""
+    import torch
+    from ensem3a_openclraytracer_amd import distributed as D
+    sc, cam, env, npix, spp, mb, ibl = W.PARITY_CASES["cornell_64_s4"].inputs()
+    full = _launch(kl, sc, cam, env, npix, spp, mb, ibl, "fast")
+    w, world = int(cam[6]), 3
+    quant = D.gpu_rgb8(kl.native)
+    tiles = [D.render_distributed(D.gpu_tile_renderer(kl.native, cam, env, npix, spp, mb), npix, w, r, world,
+                                  device="cuda", gather=False, quantize=quant) for r in range(world)]
+    torch.cuda.synchronize()
+    frame = D.assemble(tiles, w, npix, world).cpu().numpy()
+    np.testing.assert_array_equal(frame, O.rgb8(full))
+
+
+def test_save_img_through_the_device(kl, tmp_path):
+    from PIL import Image
+    from ensem3a_openclraytracer_amd import output
+    sc, cam, env, npix, spp, mb, ibl = W.PARITY_CASES["cornell_64_s4"].inputs()
+    f = _launch(kl, sc, cam, env, npix, spp, mb, ibl, "fast")
+    img = output.saveImg(f.reshape(64, 64, 3), 64, 64, str(tmp_path / "out"), launcher=kl)
+    with Image.open(tmp_path / "out.png") as im:
+        np.testing.assert_array_equal(np.asarray(im.convert("RGB")), O.rgb8(f).reshape(64, 64, 3))
+    np.testing.assert_array_equal(img, O.rgb8(f).reshape(64, 64, 3))

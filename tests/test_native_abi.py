@@ -18,7 +18,7 @@ def _declared():
     for h in ("rt_api.h", "rt_debug.h", "rt_scene.h"):
         with open(os.path.join(ROOT, "include", h)) as f:
             txt = f.read()
-        names |= set(re.findall(r"\b(rt_[a-z_]+)\s*\(", txt))
+        names |= set(re.findall(r"\b(rt_[a-z0-9_]+)\s*\(", txt))
     return names
 
 
