@@ -44,7 +44,7 @@ struct Device {
     hipStream_t stream = nullptr;
     int cus = 0;                  // compute units (sizes the FAST stack overflow buffer)
     DevBuf stack_ovf;             // FAST traversal stack entries beyond the LDS part
-    DevBuf nodes, brute, bvh9, tri_geo, tri_shade, tri_frame, mat, ibl, out, out8, counts, work, scratch_a, scratch_b;
+    DevBuf nodes, brute, brute_box, bvh9, tri_geo, tri_shade, tri_frame, mat, ibl, out, out8, counts, work, scratch_a, scratch_b;
     char* host_stage = nullptr;   // pinned staging for rt_render / rt_render_rgb8
     size_t host_stage_bytes = 0;
 };
@@ -57,6 +57,7 @@ struct HostScene {
     std::vector<float> tri_shade;  // 4 floats per triangle
     std::vector<float> mat;
     std::vector<float> brute;      // 16 floats per triangle, small scenes only (rt_internal.h DevScene::brute)
+    std::vector<float> brute_box;  // 8 floats per triangle, padded to whole groups (DevScene::brute_box)
     int32_t nbrute = 0;
     int32_t nnodes = 0, root_ref = 0, ntri = 0, nmat = 0, nbvh9 = 0, depth = 1;
     float root_box[6] = {0, 0, 0, 0, 0, 0};
@@ -76,6 +77,7 @@ struct rt_ctx {
     int brute_max = RT_BRUTE_MAX_DEFAULT;
     int resume_min = RT_RESUME_MIN_DEFAULT;
     int team = 0;  // brute-force lanes per pixel, 0 = auto
+    int max_waves = 0;  // persistent grid cap in waves per SIMD, 0 = occupancy limit
     int block = 128;
     std::string err;
 };
@@ -300,6 +302,7 @@ bool pack_fast(HostScene& hs, const float* bvh9, int64_t nn, int64_t ntri, int l
     for (int64_t t = 0; t < ntri; ++t) hs.tri_geo[12 * t + 3] = as_f32(rank[t]);
     // small scenes: brute-force records of the reachable triangles in DFS-rank order
     hs.brute.clear();
+    hs.brute_box.clear();
     hs.nbrute = 0;
     if ((int64_t)leaves.size() <= (int64_t)brute_max) {
         std::vector<int32_t> by_rank(leaves.size());
@@ -316,6 +319,21 @@ bool pack_fast(HostScene& hs, const float* bvh9, int64_t nn, int64_t ntri, int l
             r[12] = g[8]; r[13] = g[9]; r[14] = g[10]; r[15] = as_f32(t); // e2.xyz tri
         }
         hs.nbrute = (int32_t)by_rank.size();
+        // the leaf boxes again, 32 bytes each, padded with never-hit boxes to whole groups of
+        // rt::kBoxGroup (the lock-step loop loads a group with one scalar wait)
+        const size_t ng = (by_rank.size() + rt::kBoxGroup - 1) / rt::kBoxGroup * rt::kBoxGroup;
+        hs.brute_box.assign(8 * ng, 0.0f);
+        for (size_t q = 0; q < ng; ++q) {
+            float* b = hs.brute_box.data() + 8 * q;
+            if (q < by_rank.size()) {
+                const float* r = hs.brute.data() + 16 * q;          // lo.xyz hi.x | hi.yz ...
+                b[0] = r[0]; b[1] = r[3];                           // lo.x hi.x
+                b[2] = r[1]; b[3] = r[4];                           // lo.y hi.y
+                b[4] = r[2]; b[5] = r[5];                           // lo.z hi.z
+            } else {
+                for (int k = 0; k < 6; ++k) b[k] = 1e30f;           // a point far beyond any k < 1000
+            }
+        }
     }
     if (layout == RT_BVH_SAH && leaves.size() > 1) {
         std::vector<float> lb(6 * leaves.size());
@@ -342,7 +360,7 @@ void pack_checked(HostScene& hs, const float* bvh9, int64_t nb, int64_t ntri, in
                   std::string& why) {
     hs.fast_ok = (ntri > 0) ? pack_fast(hs, bvh9, nb, ntri, layout, brute_max, why) : true;
     if (ntri == 0) { hs.nnodes = 0; hs.root_ref = 0; hs.depth = 1; hs.nodes.clear(); hs.brute.clear(); hs.nbrute = 0; }
-    if (!hs.fast_ok) { hs.brute.clear(); hs.nbrute = 0; }
+    if (!hs.fast_ok) { hs.brute.clear(); hs.brute_box.clear(); hs.nbrute = 0; }
     // render kernels keep kStackLds entries in LDS and spill deeper ones to HBM; the single-ray
     // debug kernel keeps the whole stack in LDS (int2 entries, 128 lanes): depth <= 64
     if (hs.fast_ok && hs.depth > 64) {
@@ -351,6 +369,7 @@ void pack_checked(HostScene& hs, const float* bvh9, int64_t nb, int64_t ntri, in
     }
     if (hs.nodes.empty()) hs.nodes.assign(4 * rt::kNodeF4, 0.0f);
     if (hs.brute.empty()) hs.brute.assign(16, 0.0f);
+    if (hs.brute_box.empty()) hs.brute_box.assign(8 * rt::kBoxGroup, 1e30f);
 }
 
 // HBM part of the FAST traversal stack: (depth - kStackLds) entries for every lane a
@@ -388,6 +407,7 @@ rt::DevScene dev_scene(const rt_ctx* ctx, const Device& d) {
     s.ibl_h = ctx->ibl_h;
     s.depth = ctx->hs.depth;
     s.brute = (const float4*)d.brute.p;
+    s.brute_box = (const float4*)d.brute_box.p;
     s.nbrute = ctx->hs.nbrute;
     s.stack_lds = std::min<int32_t>(ctx->hs.depth > 0 ? ctx->hs.depth : 1, rt::kStackLds);
     s.stack_ovf = (int2*)d.stack_ovf.p;
@@ -416,6 +436,7 @@ int check_frame(rt_ctx* ctx, const float* cam, const float* env, int64_t npix, i
     fp->log_pixel = -1;
     fp->resume_min = ctx->resume_min;
     fp->team = ctx->team;
+    fp->max_waves = ctx->max_waves;
     fp->log_buf = nullptr;
     fp->log_cap = 0;
     fp->log_count = nullptr;
@@ -471,7 +492,7 @@ void rt_destroy(rt_ctx* ctx) {
     for (auto& d : ctx->devs) {
         if (hipSetDevice(d.id) != hipSuccess) continue;
         if (d.stream) (void)hipStreamSynchronize(d.stream);
-        for (DevBuf* b : {&d.stack_ovf, &d.nodes, &d.brute, &d.bvh9, &d.tri_geo, &d.tri_shade, &d.tri_frame, &d.mat, &d.ibl, &d.out,
+        for (DevBuf* b : {&d.stack_ovf, &d.nodes, &d.brute, &d.brute_box, &d.bvh9, &d.tri_geo, &d.tri_shade, &d.tri_frame, &d.mat, &d.ibl, &d.out,
                           &d.counts, &d.work, &d.scratch_a, &d.scratch_b})
             release(*b);
         if (d.host_stage) (void)hipHostFree(d.host_stage);
@@ -507,6 +528,7 @@ int rt_set_option(rt_ctx* ctx, const char* key, int64_t value) {
             HIP_OR_RET(ctx, hipSetDevice(d.id));
             HIP_OR_RET(ctx, upload(d.nodes, hs.nodes, d.stream));
             HIP_OR_RET(ctx, upload(d.brute, hs.brute, d.stream));
+            HIP_OR_RET(ctx, upload(d.brute_box, hs.brute_box, d.stream));
             HIP_OR_RET(ctx, upload(d.tri_geo, hs.tri_geo, d.stream));
             HIP_OR_RET(ctx, ensure_stack_ovf(d, hs));
             HIP_OR_RET(ctx, hipStreamSynchronize(d.stream));
@@ -523,6 +545,11 @@ int rt_set_option(rt_ctx* ctx, const char* key, int64_t value) {
         if (value != 0 && value != 1 && value != 2 && value != 4 && value != 8)
             return set_err(ctx, RT_ERR_ARG, "team must be 0 (auto), 1, 2, 4 or 8");
         ctx->team = (int)value;
+        return RT_OK;
+    }
+    if (!std::strcmp(key, "waves")) {
+        if (value < 0 || value > 8) return set_err(ctx, RT_ERR_ARG, "waves must be in 0..8");
+        ctx->max_waves = (int)value;
         return RT_OK;
     }
     if (!std::strcmp(key, "block")) {
@@ -617,6 +644,7 @@ int rt_set_scene(rt_ctx* ctx, const float* vp, int64_t nvp, const float* vn, int
         HIP_OR_RET(ctx, hipSetDevice(d.id));
         HIP_OR_RET(ctx, upload(d.nodes, hs.nodes, d.stream));
         HIP_OR_RET(ctx, upload(d.brute, hs.brute, d.stream));
+        HIP_OR_RET(ctx, upload(d.brute_box, hs.brute_box, d.stream));
         HIP_OR_RET(ctx, ensure_stack_ovf(d, hs));
         HIP_OR_RET(ctx, upload(d.bvh9, hs.bvh9, d.stream));
         HIP_OR_RET(ctx, upload(d.tri_geo, hs.tri_geo, d.stream));

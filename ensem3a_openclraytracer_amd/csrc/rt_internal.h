@@ -17,6 +17,11 @@ constexpr int kStackLds = RT_STACK_LDS;
 #endif
 constexpr int kNodeF4 = RT_BVH_WIDTH == 4 ? 8 : 4;
 constexpr int kMaxLanesPerCu = 2048;   // resident threads per CU (gfx950)
+// leaf boxes per scalar load group of the brute-force loop (DevScene::brute_box)
+#ifndef RT_BOX_GROUP
+#define RT_BOX_GROUP 4
+#endif
+constexpr int kBoxGroup = RT_BOX_GROUP;
 
 // Device view of one uploaded scene (all pointers are device pointers).
 struct DevScene {
@@ -54,6 +59,9 @@ struct DevScene {
     // (leaf box, a.p, e1, e2, triangle index); nbrute = 0 when the BVH path is used
     const float4* brute;
     int32_t nbrute;
+    // the same leaf boxes, 2 float4 each (lo.x hi.x lo.y hi.y | lo.z hi.z 0 0), padded to whole groups of
+    // kBoxGroup with boxes no ray reaches: the lock-step loop loads a group with one scalar wait
+    const float4* brute_box;
 };
 
 struct FrameParams {
@@ -67,6 +75,7 @@ struct FrameParams {
     int64_t nloc;        // pixels in this tile = rows * width
     int32_t resume_min;  // FAST tree walk: resumable traversal, shade once this many lanes are free (0 = off)
     int32_t team;        // brute-force path: lanes per pixel (1, 2, 4, 8; 0 = chosen at launch from the tile size)
+    int32_t max_waves;   // persistent grid: at most this many waves per SIMD (0 = as many as stay resident)
     // debug event log of one pixel (rt_debug_pixel_log only; unused by the product launches)
     int64_t log_pixel;
     float* log_buf;

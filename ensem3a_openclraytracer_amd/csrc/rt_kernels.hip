@@ -441,9 +441,6 @@ __device__ Hit trace_brute(const DevScene& S, rtm_f3 o, rtm_f3 d, Cnt& c) {
 // the minimum key is the reference's hit (lowest rank on equal distances).
 // Culling uses the owner's best as of the last batch (a conservative bound).
 constexpr int BRUTE_WAVE_LDS = 64 * 6 * 4 + 64 * 8 + 128 * 4;   // ray table | best keys | pair ring
-#ifndef RT_BRUTE_UNROLL
-#define RT_BRUTE_UNROLL 1   // box-test loop unroll (several scalar record loads in flight)
-#endif
 
 // Lanes of one wave hand data to each other through LDS here.  The hardware runs a
 // wave's LDS instructions in order; this keeps the compiler from reordering them
@@ -519,16 +516,29 @@ __device__ Hit trace_brute_compact(const DevScene& S, rtm_f3 o, rtm_f3 d, char* 
         }
     };
     if (ts == 1) {
-#pragma unroll RT_BRUTE_UNROLL
-        for (int q = 0; q < S.nbrute; ++q) {
-            if (COUNT) count_wave(c.wave_trav);
-            const ConstF4 cb = as_const(S.brute);
-            const float4 r0 = sgpr4(cb[4 * q + 0]), r1 = sgpr4(cb[4 * q + 1]);
-            float tn, tx;
-            slab_fma(r0.x, r0.w, r0.y, r1.x, r0.z, r1.y, o.x, o.y, o.z, ix, iy, iz, oix, oiy, oiz, tn, tx);
-            const bool pass = fmaxf(tn, 0.0f) <= fminf(tx, bk * CULL_MARGIN);
-            if (COUNT) c.nodes++;
-            enqueue(pass, (unsigned)q);
+        // kBoxGroup boxes per scalar wait: the group's records are loaded together (2 float4 each,
+        // padded with never-hit boxes), all its slab tests run back to back, then the passes are
+        // queued in record order (culling uses the best hit as of the group's start: conservative)
+        const ConstF4 cb = as_const(S.brute_box);
+        for (int q0 = 0; q0 < S.nbrute; q0 += kBoxGroup) {
+            float4 bx[2 * kBoxGroup];
+#pragma unroll
+            for (int j = 0; j < 2 * kBoxGroup; ++j) bx[j] = sgpr4(cb[2 * q0 + j]);
+            const float cull = bk * CULL_MARGIN;
+            bool pass[kBoxGroup];
+#pragma unroll
+            for (int j = 0; j < kBoxGroup; ++j) {
+                float tn, tx;
+                slab_fma(bx[2 * j].x, bx[2 * j].y, bx[2 * j].z, bx[2 * j].w, bx[2 * j + 1].x, bx[2 * j + 1].y, o.x,
+                         o.y, o.z, ix, iy, iz, oix, oiy, oiz, tn, tx);
+                pass[j] = fmaxf(tn, 0.0f) <= fminf(tx, cull);
+            }
+#pragma unroll
+            for (int j = 0; j < kBoxGroup; ++j) {
+                if (q0 + j >= S.nbrute) break;   // padding (never hit; skipped so the counters stay exact)
+                if (COUNT) { count_wave(c.wave_trav); c.nodes++; }
+                enqueue(pass[j], (unsigned)(q0 + j));
+            }
         }
     } else {
         const int rounds = (S.nbrute + ts - 1) / ts;
@@ -551,7 +561,8 @@ __device__ Hit trace_brute_compact(const DevScene& S, rtm_f3 o, rtm_f3 d, char* 
     Hit best{1000.0f, -1};
     if (key != nokey) {
         best.k = __uint_as_float((unsigned)(key >> 32));
-        best.tri = __float_as_int(S.brute[4 * (unsigned)(key & 0xffffffffu) + 3].w);
+        // triangle index: the record's last float4 (read from the LDS copy when it is staged)
+        best.tri = __float_as_int(mtrec[mtstride * (unsigned)(key & 0xffffffffu) + 2].w);
     }
     return best;
 }
@@ -807,6 +818,52 @@ __device__ __forceinline__ void store_pixel(float* __restrict__ out, int p, rtm_
 
 enum Phase { FETCH = 0, PRIMARY = 1, PREP = 2, BOUNCE = 3, SUN = 4, DONE = 5 };
 
+// ---- pixel hand-out ----
+// A wave keeps a private range [next, end) of tile pixels and refills it from the global counter
+// (one device-scope atomic on an address every wave of every XCD shares) only when it runs short;
+// the base comes back as a scalar, and once the counter is exhausted (`dry`) the wave never goes
+// back to it.  RT_FETCH_CHUNK > 1 reserves that many pixels per atomic; measured on C2 (1 GPU),
+// 1 is fastest (9.9 ms against 10.3-10.6 ms for 2..16: reserved pixels unbalance the end of the
+// frame).  All state is wave-uniform.  rank: the requesting lane's (or team's) rank in `need`;
+// returns its tile pixel index (>= nloc: none left).
+#ifndef RT_FETCH_CHUNK
+#define RT_FETCH_CHUNK 1
+#endif
+struct PixelQueue {
+    unsigned next = 0, end = 0;
+    bool dry = false;   // the global counter is exhausted
+};
+__device__ __forceinline__ unsigned take_pixel(PixelQueue& Q, unsigned long long need, unsigned rank,
+                                               unsigned* __restrict__ counter, unsigned nloc, int lane) {
+    const unsigned k = (unsigned)__popcll(need);
+    const unsigned avail = Q.end - Q.next;
+    if (k <= avail) {
+        const unsigned q = Q.next + rank;
+        Q.next += k;
+        return q;
+    }
+    if (Q.dry) {
+        const unsigned q = rank < avail ? Q.next + rank : nloc;
+        Q.next = Q.end;
+        return q;
+    }
+    const unsigned want = max(k - avail, (unsigned)RT_FETCH_CHUNK);
+    const int leader = __ffsll((long long)need) - 1;
+    unsigned got = 0;
+    if (lane == leader) got = atomicAdd(counter, want);
+    const unsigned nb = (unsigned)__builtin_amdgcn_readfirstlane((int)__shfl(got, leader, 64));
+    const unsigned q = rank < avail ? Q.next + rank : nb + (rank - avail);
+    if (nb >= nloc) {
+        Q.next = Q.end;
+        Q.dry = true;
+    } else {
+        Q.end = min(nb + want, nloc);
+        Q.next = min(nb + (k - avail), Q.end);
+        Q.dry = nb + want >= nloc;
+    }
+    return q;
+}
+
 // RT_MIN_WAVES: waves per SIMD the register allocator must leave room for (0 = compiler's choice).
 #ifndef RT_MIN_WAVES
 #define RT_MIN_WAVES 0
@@ -888,6 +945,7 @@ __global__ void RT_RENDER_BOUNDS render_kernel(DevScene S, FrameParams F, float*
                                              : ts == 4 ? 0x1111111111111111ull : 0x0101010101010101ull;
 
     int phase = FETCH;
+    PixelQueue pq;
     int p = 0, i = 0;
     bool logme = false;
     uint32_t seed0 = 0, seed1 = 0;
@@ -906,13 +964,9 @@ __global__ void RT_RENDER_BOUNDS render_kernel(DevScene S, FrameParams F, float*
         // teams (BRUTE, F.team lanes per pixel): one bit per team, the team's lanes take the same pixel
         const unsigned long long need = __ballot(phase == FETCH) & team_leaders;
         if (need) {
-            unsigned int base = 0;
-            const int leader = __ffsll((long long)need) - 1;
-            if (lane == leader) base = atomicAdd(work_counter, (unsigned int)__popcll(need));
-            base = __shfl(base, leader, 64);
+            const unsigned rank = (unsigned)__popcll(need & ((1ull << team_lane0) - 1ull));
+            const unsigned int q = take_pixel(pq, need, rank, work_counter, nloc, lane);
             if (phase == FETCH) {
-                const unsigned long long below = need & ((1ull << team_lane0) - 1ull);
-                const unsigned int q = base + (unsigned int)__popcll(below);
                 bool ok = q < nloc;
                 if (ok) {
                     p = (int)q;
@@ -1192,6 +1246,7 @@ __global__ void RT_RESUME_BOUNDS render_resume_kernel(DevScene S, FrameParams F,
 
     int phase = FETCH;
     bool tracing = false;
+    PixelQueue pq;
     FastRay T;
     T.item = 0; T.soff = 0; T.bk = 1000.0f; T.bt = -1; T.brank = -1;
     T.o = rtm_v3(0, 0, 0); T.d = rtm_v3(0, 0, 1); T.ix = T.iy = T.iz = 0.0f;
@@ -1232,13 +1287,9 @@ __global__ void RT_RESUME_BOUNDS render_resume_kernel(DevScene S, FrameParams F,
         // -- refill: ballot the lanes that need a pixel, one atomic per wave --
         const unsigned long long need = __ballot(phase == FETCH);
         if (need) {
-            unsigned int base = 0;
-            const int leader = __ffsll((long long)need) - 1;
-            if (lane == leader) base = atomicAdd(work_counter, (unsigned int)__popcll(need));
-            base = __shfl(base, leader, 64);
+            const unsigned rank = (unsigned)__popcll(need & ((1ull << lane) - 1ull));
+            const unsigned int q = take_pixel(pq, need, rank, work_counter, nloc, lane);
             if (phase == FETCH) {
-                const unsigned long long below = need & ((1ull << lane) - 1ull);
-                const unsigned int q = base + (unsigned int)__popcll(below);
                 bool ok = q < nloc;
                 if (ok) {
                     p = (int)q;
@@ -1444,7 +1495,9 @@ hipError_t launch_t(const DevScene& sc, const FrameParams& fp, int block, float*
                              : (const void*)render_kernel<TRAV, COUNT, LOG, SMEM, OVF, BRUTE ? 1 : 0>;
     if (e == hipSuccess) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kfn, block, lds);
     if (e != hipSuccess) return e;
-    const int64_t resident = (int64_t)std::max(1, cus) * std::max(1, per_cu);
+    // blocks per CU for at most max_waves waves per SIMD (4 SIMDs per CU)
+    const int cap_cu = fp.max_waves > 0 ? std::max(1, fp.max_waves * 4 * 64 / block) : INT_MAX;
+    const int64_t resident = (int64_t)std::max(1, cus) * std::max(1, std::min(per_cu, cap_cu));
     // brute-force teams: a tile with fewer pixels than the device has lanes (a row slice of a
     // multi-GPU frame) gives each pixel 2 or 4 lanes that split its box tests
     FrameParams f = fp;
@@ -1465,7 +1518,7 @@ hipError_t launch_t(const DevScene& sc, const FrameParams& fp, int block, float*
         int per_cu_t = 0;
         e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu_t, tfn, block, lds);
         if (e != hipSuccess) return e;
-        grid = std::min(need, (int64_t)std::max(1, cus) * std::max(1, per_cu_t));
+        grid = std::min(need, (int64_t)std::max(1, cus) * std::max(1, std::min(per_cu_t, cap_cu)));
     }
     e = hipMemsetAsync(d_work, 0, sizeof(unsigned int), stream);
     if (e != hipSuccess) return e;

@@ -222,6 +222,36 @@ def test_resumable_traversal_matches_plain_walk(kl, case):
         kl.native.set_option("resume_min", 65)
 
 
+@pytest.mark.parametrize("case", ["cornell_64_s4", "monkey_c3_64_s4"])
+def test_resident_wave_cap_renders_identically(kl, case):
+    """waves (cap on resident waves per SIMD of the persistent grid) changes which wave renders which
+    pixel and how many pixels each wave pulls from the counter -- never the frame.  Both render
+    kernels: lock-step brute force (cornell) and resumable tree walk (monkey)."""
+    sc, cam, env, npix, spp, mb, ibl = W.PARITY_CASES[case].inputs()
+    frames = []
+    try:
+        for w in (0, 1, 2, 3):
+            kl.native.set_option("waves", w)
+            frames.append(_launch(kl, sc, cam, env, npix, spp, mb, ibl, "fast"))
+    finally:
+        kl.native.set_option("waves", 0)
+    for f in frames[1:]:
+        np.testing.assert_array_equal(frames[0], f)
+    np.testing.assert_array_equal(frames[0], _oracle(sc, cam, env, npix, spp, mb, ibl))
+    with pytest.raises(_native.NativeError, match="waves"):
+        kl.native.set_option("waves", 9)
+
+
+def test_partial_last_row_matches_oracle(kl):
+    """imgDim not a multiple of the row width: the last row is partial; every pixel handed out once."""
+    wl = W.PARITY_CASES["cornell_64_s4"]
+    sc, cam, env, npix, spp, mb, ibl = wl.inputs()
+    npix = 64 * 63 + 17
+    got = _launch(kl, sc, cam, env, npix, spp, mb, ibl, "fast")
+    ref = _oracle(sc, cam, env, npix, spp, mb, ibl)   # whole rows: the pixels past npix are not rendered
+    np.testing.assert_array_equal(got, ref[: 3 * npix])
+
+
 def test_deep_tree_stack_spills_to_hbm(kl):
     """grid-1M: its SAH tree is deeper than the LDS part of the traversal stack, so
     deep entries go through the HBM overflow buffer; the frame still matches the oracle bit for bit."""
