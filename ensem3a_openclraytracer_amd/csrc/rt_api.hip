@@ -14,7 +14,9 @@
 #include <cstdarg>
 #include <cstdio>
 #include <algorithm>
+#include <array>
 #include <cstring>
+#include <map>
 #include <string>
 #include <vector>
 
@@ -59,6 +61,7 @@ struct HostScene {
     std::vector<float> brute;      // 16 floats per triangle, small scenes only (rt_internal.h DevScene::brute)
     std::vector<float> brute_box;  // 8 floats per triangle, padded to whole groups (DevScene::brute_box)
     int32_t nbrute = 0;
+    int32_t nbox = 0;              // distinct leaf boxes in brute_box (records with bit-identical boxes share one)
     int32_t nnodes = 0, root_ref = 0, ntri = 0, nmat = 0, nbvh9 = 0, depth = 1;
     float root_box[6] = {0, 0, 0, 0, 0, 0};
     bool fast_ok = false;
@@ -304,6 +307,7 @@ bool pack_fast(HostScene& hs, const float* bvh9, int64_t nn, int64_t ntri, int l
     hs.brute.clear();
     hs.brute_box.clear();
     hs.nbrute = 0;
+    hs.nbox = 0;
     if ((int64_t)leaves.size() <= (int64_t)brute_max) {
         std::vector<int32_t> by_rank(leaves.size());
         for (int32_t n : leaves) by_rank[rank[T[n]]] = n;
@@ -319,19 +323,42 @@ bool pack_fast(HostScene& hs, const float* bvh9, int64_t nn, int64_t ntri, int l
             r[12] = g[8]; r[13] = g[9]; r[14] = g[10]; r[15] = as_f32(t); // e2.xyz tri
         }
         hs.nbrute = (int32_t)by_rank.size();
-        // the leaf boxes again, 32 bytes each, padded with never-hit boxes to whole groups of
-        // rt::kBoxGroup (the lock-step loop loads a group with one scalar wait)
-        const size_t ng = (by_rank.size() + rt::kBoxGroup - 1) / rt::kBoxGroup * rt::kBoxGroup;
+        // the distinct leaf boxes, 32 bytes each: records whose leaf boxes are bit-identical (the
+        // two triangles of an axis-aligned or vertical quad) share one box test, which passes or
+        // fails for both.  Each box lists up to two records (the second -1 when alone); padded with
+        // never-hit boxes to whole groups of rt::kBoxGroup (the lock-step loop loads a group with
+        // one scalar wait).
+        std::vector<std::array<int32_t, 2>> groups;
+        {
+            std::map<std::array<uint32_t, 6>, size_t> open;   // box bits -> group with a free slot
+            for (size_t q = 0; q < by_rank.size(); ++q) {
+                const float* r = hs.brute.data() + 16 * q;
+                std::array<uint32_t, 6> key;
+                for (int k = 0; k < 6; ++k) std::memcpy(&key[k], r + k, 4);
+                auto it = open.find(key);
+                if (RT_BOX_DEDUP && it != open.end()) {
+                    groups[it->second][1] = (int32_t)q;
+                    open.erase(it);
+                } else {
+                    open[key] = groups.size();
+                    groups.push_back({(int32_t)q, -1});
+                }
+            }
+        }
+        hs.nbox = (int32_t)groups.size();
+        const size_t ng = (groups.size() + rt::kBoxGroup - 1) / rt::kBoxGroup * rt::kBoxGroup;
         hs.brute_box.assign(8 * ng, 0.0f);
-        for (size_t q = 0; q < ng; ++q) {
-            float* b = hs.brute_box.data() + 8 * q;
-            if (q < by_rank.size()) {
-                const float* r = hs.brute.data() + 16 * q;          // lo.xyz hi.x | hi.yz ...
-                b[0] = r[0]; b[1] = r[3];                           // lo.x hi.x
-                b[2] = r[1]; b[3] = r[4];                           // lo.y hi.y
-                b[4] = r[2]; b[5] = r[5];                           // lo.z hi.z
+        for (size_t g = 0; g < ng; ++g) {
+            float* b = hs.brute_box.data() + 8 * g;
+            if (g < groups.size()) {
+                const float* r = hs.brute.data() + 16 * groups[g][0];   // lo.xyz hi.x | hi.yz ...
+                b[0] = r[0]; b[1] = r[3];                                // lo.x hi.x
+                b[2] = r[1]; b[3] = r[4];                                // lo.y hi.y
+                b[4] = r[2]; b[5] = r[5];                                // lo.z hi.z
+                b[6] = as_f32(groups[g][0]); b[7] = as_f32(groups[g][1]);
             } else {
-                for (int k = 0; k < 6; ++k) b[k] = 1e30f;           // a point far beyond any k < 1000
+                for (int k = 0; k < 6; ++k) b[k] = 1e30f;                // a point far beyond any k < 1000
+                b[6] = as_f32(-1); b[7] = as_f32(-1);
             }
         }
     }
@@ -359,8 +386,11 @@ bool pack_fast(HostScene& hs, const float* bvh9, int64_t nn, int64_t ntri, int l
 void pack_checked(HostScene& hs, const float* bvh9, int64_t nb, int64_t ntri, int layout, int brute_max,
                   std::string& why) {
     hs.fast_ok = (ntri > 0) ? pack_fast(hs, bvh9, nb, ntri, layout, brute_max, why) : true;
-    if (ntri == 0) { hs.nnodes = 0; hs.root_ref = 0; hs.depth = 1; hs.nodes.clear(); hs.brute.clear(); hs.nbrute = 0; }
-    if (!hs.fast_ok) { hs.brute.clear(); hs.brute_box.clear(); hs.nbrute = 0; }
+    if (ntri == 0) {
+        hs.nnodes = 0; hs.root_ref = 0; hs.depth = 1; hs.nodes.clear();
+        hs.brute.clear(); hs.brute_box.clear(); hs.nbrute = 0; hs.nbox = 0;
+    }
+    if (!hs.fast_ok) { hs.brute.clear(); hs.brute_box.clear(); hs.nbrute = 0; hs.nbox = 0; }
     // render kernels keep kStackLds entries in LDS and spill deeper ones to HBM; the single-ray
     // debug kernel keeps the whole stack in LDS (int2 entries, 128 lanes): depth <= 64
     if (hs.fast_ok && hs.depth > 64) {
@@ -409,6 +439,7 @@ rt::DevScene dev_scene(const rt_ctx* ctx, const Device& d) {
     s.brute = (const float4*)d.brute.p;
     s.brute_box = (const float4*)d.brute_box.p;
     s.nbrute = ctx->hs.nbrute;
+    s.nbox = ctx->hs.nbox;
     s.stack_lds = std::min<int32_t>(ctx->hs.depth > 0 ? ctx->hs.depth : 1, rt::kStackLds);
     s.stack_ovf = (int2*)d.stack_ovf.p;
     return s;

@@ -22,6 +22,10 @@ constexpr int kMaxLanesPerCu = 2048;   // resident threads per CU (gfx950)
 #define RT_BOX_GROUP 4
 #endif
 constexpr int kBoxGroup = RT_BOX_GROUP;
+// brute-force records whose leaf boxes are bit-identical share one box test (DevScene::brute_box)
+#ifndef RT_BOX_DEDUP
+#define RT_BOX_DEDUP 1
+#endif
 
 // Device view of one uploaded scene (all pointers are device pointers).
 struct DevScene {
@@ -59,9 +63,11 @@ struct DevScene {
     // (leaf box, a.p, e1, e2, triangle index); nbrute = 0 when the BVH path is used
     const float4* brute;
     int32_t nbrute;
-    // the same leaf boxes, 2 float4 each (lo.x hi.x lo.y hi.y | lo.z hi.z 0 0), padded to whole groups of
-    // kBoxGroup with boxes no ray reaches: the lock-step loop loads a group with one scalar wait
+    // the distinct leaf boxes, 2 float4 each (lo.x hi.x lo.y hi.y | lo.z hi.z q0 q1): q0 (and q1 >= 0,
+    // int bits) are the records whose leaf box it is.  Padded to whole groups of kBoxGroup with boxes
+    // no ray reaches: the lock-step loop loads a group with one scalar wait
     const float4* brute_box;
+    int32_t nbox;
 };
 
 struct FrameParams {

@@ -440,7 +440,7 @@ __device__ Hit trace_brute(const DevScene& S, rtm_f3 o, rtm_f3 d, Cnt& c) {
 // (distance bits, DFS position): positive float bits order like the floats, so
 // the minimum key is the reference's hit (lowest rank on equal distances).
 // Culling uses the owner's best as of the last batch (a conservative bound).
-constexpr int BRUTE_WAVE_LDS = 64 * 6 * 4 + 64 * 8 + 128 * 4;   // ray table | best keys | pair ring
+constexpr int BRUTE_WAVE_LDS = 64 * 6 * 4 + 64 * 8 + 256 * 4;   // ray table | best keys | pair ring
 
 // Lanes of one wave hand data to each other through LDS here.  The hardware runs a
 // wave's LDS instructions in order; this keeps the compiler from reordering them
@@ -478,7 +478,7 @@ __device__ Hit trace_brute_compact(const DevScene& S, rtm_f3 o, rtm_f3 d, char* 
     unsigned head = 0, tail = 0;   // wave-uniform ring positions
     auto run_batch = [&](int n) __attribute__((always_inline)) {
         if (myrank < n) {
-            const unsigned e = ring[(head + myrank) & 127];
+            const unsigned e = ring[(head + myrank) & 255];
             const unsigned ow = e >> 16, q = e & 0xffffu;
             const rtm_f3 ro = rtm_v3(ray[ow], ray[64 + ow], ray[128 + ow]);
             const rtm_f3 rd = rtm_v3(ray[192 + ow], ray[256 + ow], ray[320 + ow]);
@@ -502,28 +502,36 @@ __device__ Hit trace_brute_compact(const DevScene& S, rtm_f3 o, rtm_f3 d, char* 
         head += n;
         wave_lds_sync();
     };
-    // queue a passing (owner, triangle) pair; run a batch once a full wave of pairs is queued
-    auto enqueue = [&](bool pass, unsigned q) __attribute__((always_inline)) {
+    // queue the passing (owner, triangle) pairs of records qa and qb (qb wave-uniform; < 0: none),
+    // which share one leaf box; run batches while a full wave of pairs is queued.  The ring holds
+    // 256 pairs: fewer than nact (<= 64) are queued before a call, which adds at most 128.
+    auto enqueue = [&](bool pass, unsigned qa, int qb) __attribute__((always_inline)) {
         const unsigned long long m = __ballot(pass);
         if (m == 0) return;
-        if (COUNT && pass) c.tris++;
-        if (pass) ring[(tail + __popcll(m & ((1ull << lane) - 1ull))) & 127] = (tl << 16) | q;
-        tail += __popcll(m);
+        const unsigned n = (unsigned)__popcll(m);
+        if (pass) {
+            if (COUNT) c.tris += qb >= 0 ? 2 : 1;
+            const unsigned r = tail + (unsigned)__popcll(m & ((1ull << lane) - 1ull));
+            ring[r & 255] = (tl << 16) | qa;
+            if (qb >= 0) ring[(r + n) & 255] = (tl << 16) | (unsigned)qb;
+        }
+        tail += qb >= 0 ? 2 * n : n;
         wave_lds_sync();
         if ((int)(tail - head) >= nact) {
-            run_batch(nact);
+            do run_batch(nact); while ((int)(tail - head) >= nact);
             bk = __uint_as_float((unsigned)(bestk[tl] >> 32));
         }
     };
     if (ts == 1) {
-        // kBoxGroup boxes per scalar wait: the group's records are loaded together (2 float4 each,
-        // padded with never-hit boxes), all its slab tests run back to back, then the passes are
-        // queued in record order (culling uses the best hit as of the group's start: conservative)
+        // kBoxGroup distinct leaf boxes per scalar wait: the group is loaded together (2 float4 per box:
+        // the box and its one or two records; padded with never-hit boxes), all its slab tests run back
+        // to back, then the passes are queued (culling uses the best hit as of the group's start:
+        // conservative)
         const ConstF4 cb = as_const(S.brute_box);
-        for (int q0 = 0; q0 < S.nbrute; q0 += kBoxGroup) {
+        for (int g0 = 0; g0 < S.nbox; g0 += kBoxGroup) {
             float4 bx[2 * kBoxGroup];
 #pragma unroll
-            for (int j = 0; j < 2 * kBoxGroup; ++j) bx[j] = sgpr4(cb[2 * q0 + j]);
+            for (int j = 0; j < 2 * kBoxGroup; ++j) bx[j] = sgpr4(cb[2 * g0 + j]);
             const float cull = bk * CULL_MARGIN;
             bool pass[kBoxGroup];
 #pragma unroll
@@ -535,25 +543,35 @@ __device__ Hit trace_brute_compact(const DevScene& S, rtm_f3 o, rtm_f3 d, char* 
             }
 #pragma unroll
             for (int j = 0; j < kBoxGroup; ++j) {
-                if (q0 + j >= S.nbrute) break;   // padding (never hit; skipped so the counters stay exact)
-                if (COUNT) { count_wave(c.wave_trav); c.nodes++; }
-                enqueue(pass[j], (unsigned)(q0 + j));
+                if (g0 + j >= S.nbox) break;   // padding (never hit; skipped so the counters stay exact)
+                const int qa = __float_as_int(bx[2 * j + 1].z), qb = __float_as_int(bx[2 * j + 1].w);
+                if (COUNT) {   // counted per record (one leaf box test each, as in the tree walk)
+                    count_wave(c.wave_trav); c.nodes++;
+                    if (qb >= 0) { count_wave(c.wave_trav); c.nodes++; }
+                }
+                enqueue(pass[j], (unsigned)qa, qb);
             }
         }
     } else {
-        const int rounds = (S.nbrute + ts - 1) / ts;
-        for (int qq = 0; qq < rounds; ++qq) {
-            if (COUNT) count_wave(c.wave_trav);
-            const int q = qq * ts + (int)sub;
+        // box g = gg * ts + sub of each round (LDS copy of brute_box at boxrec); its second record, when
+        // there is one, differs between the lanes of the wave: queued by a second call
+        const int rounds = (S.nbox + ts - 1) / ts;
+        for (int gg = 0; gg < rounds; ++gg) {
+            if (COUNT) { count_wave(c.wave_trav); count_wave(c.wave_trav); }
+            const int g = gg * ts + (int)sub;
             bool pass = false;
-            if (q < S.nbrute) {
-                const float4 r0 = boxrec[q], r1 = mtrec[mtstride * q];
+            int qa = 0, qb = -1;
+            if (g < S.nbox) {
+                const float4 b0 = boxrec[2 * g], b1 = boxrec[2 * g + 1];
                 float tn, tx;
-                slab_fma(r0.x, r0.w, r0.y, r1.x, r0.z, r1.y, o.x, o.y, o.z, ix, iy, iz, oix, oiy, oiz, tn, tx);
+                slab_fma(b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, o.x, o.y, o.z, ix, iy, iz, oix, oiy, oiz, tn, tx);
                 pass = fmaxf(tn, 0.0f) <= fminf(tx, bk * CULL_MARGIN);
-                if (COUNT) c.nodes++;
+                qa = __float_as_int(b1.z);
+                qb = __float_as_int(b1.w);
+                if (COUNT) c.nodes += qb >= 0 ? 2 : 1;
             }
-            enqueue(pass, (unsigned)q);
+            enqueue(pass, (unsigned)qa, -1);
+            enqueue(pass && qb >= 0, (unsigned)qb, -1);
         }
     }
     while (tail != head) run_batch(min((int)(tail - head), nact));
@@ -899,12 +917,12 @@ __global__ void RT_RENDER_BOUNDS render_kernel(DevScene S, FrameParams F, float*
     const float* tmat = S.mat;
     if (BRUTE) {
         float4* lr = reinterpret_cast<float4*>(reinterpret_cast<char*>(lds_stack) + (B / 64) * BRUTE_WAVE_LDS);
-        float4* lb = lr + 3 * S.nbrute;                  // lo.xyz hi.x of each record (team box tests)
+        float4* lb = lr + 3 * S.nbrute;                  // the distinct leaf boxes (team box tests)
         if (BRUTE == 2) {
-            for (int q = threadIdx.x; q < S.nbrute; q += B) lb[q] = S.brute[4 * q];
+            for (int q = threadIdx.x; q < 2 * S.nbox; q += B) lb[q] = S.brute_box[q];
             boxrec = lb;
         }
-        float4* ls = lb + S.nbrute;
+        float4* ls = lb + 2 * S.nbox;
         float4* lf = ls + S.ntri;
         float* lm = reinterpret_cast<float*>(lf + 3 * S.ntri);
         for (int q = threadIdx.x; q < 3 * S.nbrute; q += B) lr[q] = S.brute[4 * (q / 3) + 1 + q % 3];
@@ -1483,8 +1501,8 @@ hipError_t launch_t(const DevScene& sc, const FrameParams& fp, int block, float*
     if (TRAV == TRAV_FAST && sc.nbrute > 0 && RT_BRUTE_COMPACT)
         lds = std::max(lds, (size_t)(block / 64) * BRUTE_WAVE_LDS);
     if (BRUTE)
-        lds = (size_t)(block / 64) * BRUTE_WAVE_LDS + (size_t)sc.nbrute * 64 + (size_t)sc.ntri * 64 +
-              (size_t)sc.nmat * 24;
+        lds = (size_t)(block / 64) * BRUTE_WAVE_LDS + (size_t)sc.nbrute * 48 + (size_t)sc.nbox * 32 +
+              (size_t)sc.ntri * 64 + (size_t)sc.nmat * 24;
     if (SMEM) lds += (size_t)(kNodeF4 * sc.nnodes + 3 * sc.ntri) * sizeof(float4);
     if (fp.nloc <= 0) return hipSuccess;
     // persistent grid: as many blocks as the device keeps resident (pixels are handed out by d_work)
@@ -1631,8 +1649,8 @@ hipError_t launch_fast(const DevScene& sc, const FrameParams& fp, int block, flo
         return launch_t<TRAV_FAST, COUNT, false, false, true>(sc, fp, block, d_out, d_counts, d_work, stream);
     }
     // BRUTE stages the scene in LDS: only while two blocks still fit a CU
-    const size_t brute_lds = (size_t)(block / 64) * BRUTE_WAVE_LDS + (size_t)sc.nbrute * 64 +
-                             (size_t)sc.ntri * 64 + (size_t)sc.nmat * 24;
+    const size_t brute_lds = (size_t)(block / 64) * BRUTE_WAVE_LDS + (size_t)sc.nbrute * 48 +
+                             (size_t)sc.nbox * 32 + (size_t)sc.ntri * 64 + (size_t)sc.nmat * 24;
     if (sc.ntri > 0 && sc.nbrute > 0 && RT_BRUTE_COMPACT && RT_BRUTE_LDS && brute_lds <= 80 * 1024)
         return launch_t<TRAV_FAST, COUNT, false, false, false, false, true>(sc, fp, block, d_out, d_counts, d_work,
                                                                             stream);
