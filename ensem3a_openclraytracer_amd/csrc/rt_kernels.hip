@@ -167,6 +167,8 @@ constexpr float CULL_MARGIN = 1.0f + 0x1p-12f;
 #define RT_HIT3 1
 #endif
 
+__device__ __forceinline__ bool mt_vals(float4 g0, float4 g1, float4 g2, rtm_f3 o, rtm_f3 d, float* kout, int* rank);
+
 // Branch-free Moller-Trumbore (same arithmetic as mt_test): all three loads are
 // issued together and one predicate decides, so a wave pays one memory round trip
 // and no nested divergence per triangle.
@@ -176,6 +178,11 @@ __device__ __forceinline__ bool mt_flat(const char* __restrict__ tb, unsigned to
     const float4 g0 = *reinterpret_cast<const float4*>(tb + toff);
     const float4 g1 = *reinterpret_cast<const float4*>(tb + toff + 16);
     const float4 g2 = *reinterpret_cast<const float4*>(tb + toff + 32);
+    return mt_vals(g0, g1, g2, o, d, kout, rank);
+}
+
+// mt_flat on a loaded record (g0 = a.p | rank, g1 = e1, g2 = e2).
+__device__ __forceinline__ bool mt_vals(float4 g0, float4 g1, float4 g2, rtm_f3 o, rtm_f3 d, float* kout, int* rank) {
     const rtm_f3 e1 = xyz(g1), e2 = xyz(g2);
     const rtm_f3 h = rtm_cross(d, e2);
     const float a = rtm_dot(e1, h);
@@ -228,6 +235,13 @@ __device__ __forceinline__ LaneStack lane_stack(const DevScene& S, int* lds_base
     return st;
 }
 
+#if RT_BVH_WIDTH != 4
+template <bool OVF>
+__device__ __forceinline__ int node_pick(float4 a, float4 b, float4 z, int2 e, rtm_f3 o, float ix, float iy,
+                                         float iz, float oix, float oiy, float oiz, float cull, const LaneStack& st,
+                                         unsigned& soff);
+#endif
+
 // One FAST node: test every child box against the ray, push the hit children
 // except the nearest (farthest first, with their entry distance), and return the
 // nearest hit child, or INT_MIN when none is hit (pop next).  np: the node (AoS:
@@ -276,6 +290,17 @@ __device__ __forceinline__ int node_step(const char* np, unsigned kstride, rtm_f
     const float4 b = *reinterpret_cast<const float4*>(np + kstride);
     const float4 z = *reinterpret_cast<const float4*>(np + 2 * kstride);
     const int2 e = *reinterpret_cast<const int2*>(np + 3 * kstride);
+    return node_pick<OVF>(a, b, z, e, o, ix, iy, iz, oix, oiy, oiz, cull, st, soff);
+#endif
+}
+
+#if RT_BVH_WIDTH != 4
+// The BVH2 node step on a loaded node: a / b = (lo.x hi.x lo.y hi.y) of child 0 / 1, z = (lo.z hi.z)
+// of both, e = the child refs.
+template <bool OVF>
+__device__ __forceinline__ int node_pick(float4 a, float4 b, float4 z, int2 e, rtm_f3 o, float ix, float iy,
+                                         float iz, float oix, float oiy, float oiz, float cull, const LaneStack& st,
+                                         unsigned& soff) {
     float t0n, t0x, t1n, t1x;
     slab_fma(a.x, a.y, a.z, a.w, z.x, z.y, o.x, o.y, o.z, ix, iy, iz, oix, oiy, oiz, t0n, t0x);
     slab_fma(b.x, b.y, b.z, b.w, z.z, z.w, o.x, o.y, o.z, ix, iy, iz, oix, oiy, oiz, t1n, t1x);
@@ -295,8 +320,8 @@ __device__ __forceinline__ int node_step(const char* np, unsigned kstride, rtm_f
     }
     if (h0 || h1) return h0 ? e.x : e.y;
     return INT_MIN;
-#endif
 }
+#endif
 
 // One item per iteration: an internal node (both child boxes tested, nearer hit
 // child continues, the farther is pushed with its entry distance) or a leaf
@@ -1221,6 +1246,59 @@ __device__ __forceinline__ bool fast_round(const DevScene& S, FastRay& R, const 
     return true;
 }
 
+// One item of trace_fast's loop per call (RT_STEP_UNIFIED): an internal node or a leaf, then a pop
+// when the item yields no next item.  The per-lane sequence of node steps, leaf tests and pops is
+// trace_fast's, so the hit is the same.  Every tracing lane fetches its item with the SAME four
+// vector loads, whether it is a node (64 B: both child boxes + refs) or a triangle (48 B: a.p | rank,
+// e1, e2; the fourth load re-reads its first bytes), so a wave issues 4 load instructions per step
+// with all its tracing lanes active.  On C3 the texture address unit was 89 % busy with the
+// descend-until-leaf rounds of fast_round, whose loads ran with few lanes active.
+// Returns true when the ray is finished.
+template <bool COUNT, bool SOA, bool OVF>
+__device__ __forceinline__ bool fast_step(const DevScene& S, FastRay& R, const char* nb, const char* tb,
+                                          const LaneStack& st, unsigned kstride, Cnt& c) {
+#if RT_BVH_WIDTH != 4
+    const bool node = R.item >= 0;
+    const char* p = node ? nb + (SOA ? 16u : 16u * kNodeF4) * (unsigned)R.item : tb + ~(unsigned)R.item;
+    const unsigned ks = node ? kstride : 16u;
+    const float4 g0 = *reinterpret_cast<const float4*>(p);
+    const float4 g1 = *reinterpret_cast<const float4*>(p + ks);
+    const float4 g2 = *reinterpret_cast<const float4*>(p + 2 * ks);
+    const int2 e = *reinterpret_cast<const int2*>(p + (node ? 3 * ks : 0u));
+    if (COUNT) count_wave(c.wave_trav);
+    if (node) {
+        if (COUNT) c.nodes++;
+        const float oix = R.o.x * R.ix, oiy = R.o.y * R.iy, oiz = R.o.z * R.iz;
+        R.item = node_pick<OVF>(g0, g1, g2, e, R.o, R.ix, R.iy, R.iz, oix, oiy, oiz, R.bk * CULL_MARGIN, st, R.soff);
+        if (R.item != INT_MIN) return false;
+    } else {
+        if (COUNT) c.tris++;
+        float k;
+        int rank;
+        if (mt_vals(g0, g1, g2, R.o, R.d, &k, &rank) && k > 0.0001f && (k < R.bk || (k == R.bk && rank < R.brank))) {
+            R.bk = k;
+            R.bt = (int)~(unsigned)R.item;
+            R.brank = rank;
+        }
+    }
+    while (R.soff > 0) {   // pop the next item still in front of the best hit
+        R.soff -= st.stride;
+        const int2 en = st.template get<OVF>(R.soff);
+        if (__int_as_float(en.y) <= R.bk * CULL_MARGIN) {
+            R.item = en.x;
+            return false;
+        }
+    }
+    return true;
+#else
+    return fast_round<COUNT, SOA, OVF>(S, R, nb, tb, st, kstride, c);
+#endif
+}
+
+#ifndef RT_STEP_UNIFIED
+#define RT_STEP_UNIFIED 1
+#endif
+
 #ifndef RT_RESUME_MIN_WAVES
 #define RT_RESUME_MIN_WAVES 0
 #endif
@@ -1439,7 +1517,9 @@ __global__ void RT_RESUME_BOUNDS render_resume_kernel(DevScene S, FrameParams F,
             if (lane == 0) c.cyc_shade += t_mid - t_iter;
         }
         while (true) {
-            if (tracing && fast_round<COUNT, SMEM, OVF>(S, T, nb, tb, lst, kstride, c)) tracing = false;
+            if (tracing && (RT_STEP_UNIFIED ? fast_step<COUNT, SMEM, OVF>(S, T, nb, tb, lst, kstride, c)
+                                            : fast_round<COUNT, SMEM, OVF>(S, T, nb, tb, lst, kstride, c)))
+                tracing = false;
             const unsigned long long tr = __ballot(tracing);
             if (tr == 0 || 64 - __popcll(tr) >= F.resume_min) break;
         }
