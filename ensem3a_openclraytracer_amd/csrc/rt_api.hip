@@ -617,7 +617,9 @@ int rt_set_scene(rt_ctx* ctx, const float* vp, int64_t nvp, const float* vn, int
     hs.ntri = (int32_t)T;
     hs.nmat = (int32_t)M;
     hs.nbvh9 = (int32_t)NB;
-    hs.mat.assign(mat, mat + nmat);
+    hs.mat.assign((size_t)rt::kMatF * M, 0.0f);   // rows padded to kMatF floats (DevScene::mat)
+    for (int64_t m = 0; m < M; ++m)
+        for (int k = 0; k < 6; ++k) hs.mat[(size_t)rt::kMatF * m + k] = mat[6 * m + k];
     if (bvh9) hs.bvh9.assign(bvh9, bvh9 + nbvh);
     hs.tri_geo.assign((size_t)T * 12, 0.0f);
     hs.tri_shade.assign((size_t)T * 4, 0.0f);

@@ -22,6 +22,7 @@ constexpr int kMaxLanesPerCu = 2048;   // resident threads per CU (gfx950)
 #define RT_BOX_GROUP 4
 #endif
 constexpr int kBoxGroup = RT_BOX_GROUP;
+constexpr int kMatF = 8;   // floats per device material row (DevScene::mat)
 // brute-force records whose leaf boxes are bit-identical share one box test (DevScene::brute_box)
 #ifndef RT_BOX_DEDUP
 #define RT_BOX_DEDUP 1
@@ -48,7 +49,7 @@ struct DevScene {
     // hemisphere frame per triangle (prep_frames_kernel): q, qinv, normalize(n) | colinear flag
     const float4* tri_frame;
     int32_t ntri;
-    // materials: 6 floats each [type, r, g, b, roughness, ior]
+    // materials: the reference's 6 floats [type, r, g, b, roughness, ior] padded to kMatF = 8 (two float4)
     const float* mat;
     int32_t nmat;
     // IBL RGBA8

@@ -796,12 +796,14 @@ struct Mat {
     float rough;
 };
 
+// Device material rows are padded to kMatF = 8 floats (rt_internal.h DevScene::mat): two vector loads.
 __device__ __forceinline__ Mat load_mat(const float* __restrict__ m, int idx) {
-    const float* p = m + 6 * idx;
+    const float4 a = reinterpret_cast<const float4*>(m)[2 * idx];
+    const float rough = m[kMatF * idx + 4];
     Mat r;
-    r.type = (int)p[0];
-    r.color = rtm_v3(p[1], p[2], p[3]);
-    r.rough = p[4];
+    r.type = (int)a.x;
+    r.color = rtm_v3(a.y, a.z, a.w);
+    r.rough = rough;
     return r;
 }
 
@@ -814,7 +816,7 @@ __global__ void prep_frames_kernel(const float4* __restrict__ tri_shade, const f
     if (t >= ntri) return;
     const float4 sh = tri_shade[t];
     const rtm_f3 n = xyz(sh);
-    const int type = (int)mat[6 * __float_as_int(sh.w)];
+    const int type = (int)mat[kMatF * __float_as_int(sh.w)];
     const rtm_f3 nn = rtm_normalize(n);
     const float colinear = rtm_fabs(rtm_dot(nn, rtm_v3(0.0f, 0.0f, 1.0f)));
     rtm_rot R;
@@ -953,7 +955,7 @@ __global__ void RT_RENDER_BOUNDS render_kernel(DevScene S, FrameParams F, float*
         for (int q = threadIdx.x; q < 3 * S.nbrute; q += B) lr[q] = S.brute[4 * (q / 3) + 1 + q % 3];
         for (int q = threadIdx.x; q < S.ntri; q += B) ls[q] = S.tri_shade[q];
         for (int q = threadIdx.x; q < 3 * S.ntri; q += B) lf[q] = S.tri_frame[q];
-        for (int q = threadIdx.x; q < 6 * S.nmat; q += B) lm[q] = S.mat[q];
+        for (int q = threadIdx.x; q < kMatF * S.nmat; q += B) lm[q] = S.mat[q];
         __syncthreads();
         mtrec = lr;
         tshade = ls;
@@ -1582,7 +1584,7 @@ hipError_t launch_t(const DevScene& sc, const FrameParams& fp, int block, float*
         lds = std::max(lds, (size_t)(block / 64) * BRUTE_WAVE_LDS);
     if (BRUTE)
         lds = (size_t)(block / 64) * BRUTE_WAVE_LDS + (size_t)sc.nbrute * 48 + (size_t)sc.nbox * 32 +
-              (size_t)sc.ntri * 64 + (size_t)sc.nmat * 24;
+              (size_t)sc.ntri * 64 + (size_t)sc.nmat * (4 * kMatF);
     if (SMEM) lds += (size_t)(kNodeF4 * sc.nnodes + 3 * sc.ntri) * sizeof(float4);
     if (fp.nloc <= 0) return hipSuccess;
     // persistent grid: as many blocks as the device keeps resident (pixels are handed out by d_work)
@@ -1730,7 +1732,7 @@ hipError_t launch_fast(const DevScene& sc, const FrameParams& fp, int block, flo
     }
     // BRUTE stages the scene in LDS: only while two blocks still fit a CU
     const size_t brute_lds = (size_t)(block / 64) * BRUTE_WAVE_LDS + (size_t)sc.nbrute * 48 +
-                             (size_t)sc.nbox * 32 + (size_t)sc.ntri * 64 + (size_t)sc.nmat * 24;
+                             (size_t)sc.nbox * 32 + (size_t)sc.ntri * 64 + (size_t)sc.nmat * (4 * kMatF);
     if (sc.ntri > 0 && sc.nbrute > 0 && RT_BRUTE_COMPACT && RT_BRUTE_LDS && brute_lds <= 80 * 1024)
         return launch_t<TRAV_FAST, COUNT, false, false, false, false, true>(sc, fp, block, d_out, d_counts, d_work,
                                                                             stream);
