@@ -81,6 +81,7 @@ struct rt_ctx {
     int resume_min = RT_RESUME_MIN_DEFAULT;
     int team = 0;  // brute-force lanes per pixel, 0 = auto
     int max_waves = 0;  // persistent grid cap in waves per SIMD, 0 = occupancy limit
+    int step = 0;       // tree-walk traversal loop: 0 auto, 1 one item per step, 2 descend-until-leaf rounds
     int block = 128;
     std::string err;
 };
@@ -466,6 +467,7 @@ int check_frame(rt_ctx* ctx, const float* cam, const float* env, int64_t npix, i
     fp->nloc = rt_tile_rows(npix, fp->width, row0, row_step) * fp->width;
     fp->log_pixel = -1;
     fp->resume_min = ctx->resume_min;
+    fp->step = ctx->step;
     fp->team = ctx->team;
     fp->max_waves = ctx->max_waves;
     fp->log_buf = nullptr;
@@ -576,6 +578,11 @@ int rt_set_option(rt_ctx* ctx, const char* key, int64_t value) {
         if (value != 0 && value != 1 && value != 2 && value != 4 && value != 8)
             return set_err(ctx, RT_ERR_ARG, "team must be 0 (auto), 1, 2, 4 or 8");
         ctx->team = (int)value;
+        return RT_OK;
+    }
+    if (!std::strcmp(key, "step")) {
+        if (value < 0 || value > 2) return set_err(ctx, RT_ERR_ARG, "step must be 0 (auto), 1 (item) or 2 (round)");
+        ctx->step = (int)value;
         return RT_OK;
     }
     if (!std::strcmp(key, "waves")) {

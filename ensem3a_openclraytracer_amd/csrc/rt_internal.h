@@ -83,6 +83,7 @@ struct FrameParams {
     int32_t resume_min;  // FAST tree walk: resumable traversal, shade once this many lanes are free (0 = off)
     int32_t team;        // brute-force path: lanes per pixel (1, 2, 4, 8; 0 = chosen at launch from the tile size)
     int32_t max_waves;   // persistent grid: at most this many waves per SIMD (0 = as many as stay resident)
+    int32_t step;        // FAST tree walk: 1 = one item per traversal step, 2 = descend-until-leaf rounds, 0 = auto
     // debug event log of one pixel (rt_debug_pixel_log only; unused by the product launches)
     int64_t log_pixel;
     float* log_buf;

@@ -1297,8 +1297,12 @@ __device__ __forceinline__ bool fast_step(const DevScene& S, FastRay& R, const c
 #endif
 }
 
-#ifndef RT_STEP_UNIFIED
-#define RT_STEP_UNIFIED 1
+// FrameParams::step = 0 (auto): one item per step (fast_step) when the node array is at most this
+// many bytes (L2-resident scenes, bound by the texture-address unit), descend-until-leaf rounds
+// (fast_round) above (C5's 64 MB: bound by the latency of L2 misses; fast_round 1000 vs fast_step
+// 944 Msamples/s there)
+#ifndef RT_STEP_MAX_BYTES
+#define RT_STEP_MAX_BYTES (16u << 20)
 #endif
 
 #ifndef RT_RESUME_MIN_WAVES
@@ -1310,7 +1314,7 @@ __device__ __forceinline__ bool fast_step(const DevScene& S, FastRay& R, const c
 #define RT_RESUME_BOUNDS __launch_bounds__(256)
 #endif
 
-template <bool COUNT, bool LOG, bool SMEM, bool OVF>
+template <bool COUNT, bool LOG, bool SMEM, bool OVF, bool STEP>
 __global__ void RT_RESUME_BOUNDS render_resume_kernel(DevScene S, FrameParams F, float* __restrict__ out,
                                                       unsigned long long* __restrict__ counts,
                                                       unsigned int* __restrict__ work_counter,
@@ -1519,8 +1523,8 @@ __global__ void RT_RESUME_BOUNDS render_resume_kernel(DevScene S, FrameParams F,
             if (lane == 0) c.cyc_shade += t_mid - t_iter;
         }
         while (true) {
-            if (tracing && (RT_STEP_UNIFIED ? fast_step<COUNT, SMEM, OVF>(S, T, nb, tb, lst, kstride, c)
-                                            : fast_round<COUNT, SMEM, OVF>(S, T, nb, tb, lst, kstride, c)))
+            if (tracing && (STEP ? fast_step<COUNT, SMEM, OVF>(S, T, nb, tb, lst, kstride, c)
+                                 : fast_round<COUNT, SMEM, OVF>(S, T, nb, tb, lst, kstride, c)))
                 tracing = false;
             const unsigned long long tr = __ballot(tracing);
             if (tr == 0 || 64 - __popcll(tr) >= F.resume_min) break;
@@ -1574,7 +1578,7 @@ __global__ void rgb8_kernel(const float* __restrict__ in, uint8_t* __restrict__ 
 }
 
 template <int TRAV, bool COUNT, bool LOG, bool SMEM = false, bool RESUME = false, bool OVF = false,
-          bool BRUTE = false>
+          bool BRUTE = false, bool STEP = true>
 hipError_t launch_t(const DevScene& sc, const FrameParams& fp, int block, float* d_out, unsigned long long* d_counts,
                     unsigned int* d_work, hipStream_t stream) {
     // FAST: int2 entries; the brute-force path of small scenes needs no stack
@@ -1591,7 +1595,7 @@ hipError_t launch_t(const DevScene& sc, const FrameParams& fp, int block, float*
     int dev = 0, cus = 0, per_cu = 0;
     hipError_t e = hipGetDevice(&dev);
     if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    const void* kfn = RESUME ? (const void*)render_resume_kernel<COUNT, LOG, SMEM, OVF>
+    const void* kfn = RESUME ? (const void*)render_resume_kernel<COUNT, LOG, SMEM, OVF, STEP>
                              : (const void*)render_kernel<TRAV, COUNT, LOG, SMEM, OVF, BRUTE ? 1 : 0>;
     if (e == hipSuccess) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kfn, block, lds);
     if (e != hipSuccess) return e;
@@ -1626,7 +1630,7 @@ hipError_t launch_t(const DevScene& sc, const FrameParams& fp, int block, float*
     LaunchConst* lc = reinterpret_cast<LaunchConst*>(reinterpret_cast<char*>(d_work) + 64);
     hipLaunchKernelGGL(make_const_kernel, dim3(1), dim3(64), 0, stream, f, lc);
     if (RESUME)
-        hipLaunchKernelGGL((render_resume_kernel<COUNT, LOG, SMEM, OVF>), dim3((unsigned)grid), dim3(block), lds, stream,
+        hipLaunchKernelGGL((render_resume_kernel<COUNT, LOG, SMEM, OVF, STEP>), dim3((unsigned)grid), dim3(block), lds, stream,
                            sc, f, d_out, d_counts, d_work, (const LaunchConst*)lc);
     else if (BRUTE && f.team > 1)
         hipLaunchKernelGGL((render_kernel<TRAV, COUNT, LOG, SMEM, OVF, BRUTE ? 2 : 0>), dim3((unsigned)grid),
@@ -1716,6 +1720,19 @@ hipError_t launch_debug_trace(const DevScene& sc, int traversal, const float* ra
     return hipGetLastError();
 }
 
+template <bool COUNT, bool STEP>
+hipError_t launch_resume(const DevScene& sc, const FrameParams& fp, int block, float* d_out,
+                         unsigned long long* d_counts, unsigned int* d_work, hipStream_t stream, bool smem, bool ovf) {
+    if (smem)
+        return launch_t<TRAV_FAST, COUNT, false, true, true, false, false, STEP>(sc, fp, block, d_out, d_counts,
+                                                                                 d_work, stream);
+    if (ovf)
+        return launch_t<TRAV_FAST, COUNT, false, false, true, true, false, STEP>(sc, fp, block, d_out, d_counts,
+                                                                                 d_work, stream);
+    return launch_t<TRAV_FAST, COUNT, false, false, true, false, false, STEP>(sc, fp, block, d_out, d_counts, d_work,
+                                                                              stream);
+}
+
 template <bool COUNT>
 hipError_t launch_fast(const DevScene& sc, const FrameParams& fp, int block, float* d_out,
                        unsigned long long* d_counts, unsigned int* d_work, hipStream_t stream) {
@@ -1724,11 +1741,10 @@ hipError_t launch_fast(const DevScene& sc, const FrameParams& fp, int block, flo
     const bool ovf = sc.nbrute == 0 && sc.stack_lds < sc.depth;
     const bool resume = sc.ntri > 0 && sc.nbrute == 0 && fp.resume_min > 0;
     if (resume) {
-        if (smem) return launch_t<TRAV_FAST, COUNT, false, true, true>(sc, fp, block, d_out, d_counts, d_work, stream);
-        if (ovf)
-            return launch_t<TRAV_FAST, COUNT, false, false, true, true>(sc, fp, block, d_out, d_counts, d_work,
-                                                                          stream);
-        return launch_t<TRAV_FAST, COUNT, false, false, true>(sc, fp, block, d_out, d_counts, d_work, stream);
+        const bool step = fp.step == 1 ||
+                          (fp.step == 0 && (size_t)sc.nnodes * kNodeF4 * 16 <= (size_t)RT_STEP_MAX_BYTES);
+        return step ? launch_resume<COUNT, true>(sc, fp, block, d_out, d_counts, d_work, stream, smem, ovf)
+                    : launch_resume<COUNT, false>(sc, fp, block, d_out, d_counts, d_work, stream, smem, ovf);
     }
     // BRUTE stages the scene in LDS: only while two blocks still fit a CU
     const size_t brute_lds = (size_t)(block / 64) * BRUTE_WAVE_LDS + (size_t)sc.nbrute * 48 +

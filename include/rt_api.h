@@ -79,7 +79,11 @@ int rt_set_env(rt_ctx* ctx, const uint8_t* rgba, int w, int h);
  * "resume_min" (FAST tree walk: 0 = each wave traces until all its rays are
  * done; 1..64 = rays keep their traversal state across render-loop
  * iterations and the wave shades as soon as this many lanes are free -- same
- * hits), "block" (threads per block: 64, 128 or 256).
+ * hits), "step" (resumable tree walk: 1 = one node or leaf per traversal
+ * step, 2 = descend to a leaf per step, 0 = auto by node-array size -- same
+ * hits), "team" (brute force: lanes per pixel 1/2/4/8, 0 = auto by tile
+ * size), "waves" (persistent grid: at most this many waves per SIMD, 0 =
+ * occupancy limit), "block" (threads per block: 64, 128 or 256).
  * "bvh" and "brute_max" may be changed after rt_set_scene. */
 int rt_set_option(rt_ctx* ctx, const char* key, int64_t value);
 

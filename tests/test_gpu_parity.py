@@ -222,6 +222,24 @@ def test_resumable_traversal_matches_plain_walk(kl, case):
         kl.native.set_option("resume_min", 65)
 
 
+@pytest.mark.parametrize("case", ["monkey_c3_64_s4", "serre_96x54_s4", "proto_64_s4", "furnace_64_s4"])
+def test_traversal_step_modes_render_identically(kl, case):
+    """step: one node-or-leaf item per traversal step (same four loads for both) or descend-until-leaf
+    rounds -- the same per-ray sequence of node steps, leaf tests and pops, so the same frame."""
+    sc, cam, env, npix, spp, mb, ibl = W.PARITY_CASES[case].inputs()
+    frames = []
+    try:
+        for mode in (1, 2, 0):
+            kl.native.set_option("step", mode)
+            frames.append(_launch(kl, sc, cam, env, npix, spp, mb, ibl, "fast"))
+    finally:
+        kl.native.set_option("step", 0)
+    for f in frames[1:]:
+        np.testing.assert_array_equal(frames[0], f)
+    with pytest.raises(_native.NativeError, match="step"):
+        kl.native.set_option("step", 3)
+
+
 @pytest.mark.parametrize("case", ["cornell_64_s4", "monkey_c3_64_s4"])
 def test_resident_wave_cap_renders_identically(kl, case):
     """waves (cap on resident waves per SIMD of the persistent grid) changes which wave renders which
