@@ -65,6 +65,7 @@ struct HostScene {
     int32_t nnodes = 0, root_ref = 0, ntri = 0, nmat = 0, nbvh9 = 0, depth = 1;
     float root_box[6] = {0, 0, 0, 0, 0, 0};
     bool fast_ok = false;
+    bool colors_finite = true;     // every material colour finite (FrameParams::sun_skip)
 };
 
 }  // namespace
@@ -82,6 +83,7 @@ struct rt_ctx {
     int team = 0;  // brute-force lanes per pixel, 0 = auto
     int max_waves = 0;  // persistent grid cap in waves per SIMD, 0 = occupancy limit
     int step = 0;       // tree-walk traversal loop: 0 auto, 1 one item per step, 2 descend-until-leaf rounds
+    int sun_skip = 1;   // FAST: do not trace shadow rays of an unlit sun (FrameParams::sun_skip)
     int block = 128;
     std::string err;
 };
@@ -468,6 +470,7 @@ int check_frame(rt_ctx* ctx, const float* cam, const float* env, int64_t npix, i
     fp->log_pixel = -1;
     fp->resume_min = ctx->resume_min;
     fp->step = ctx->step;
+    fp->sun_skip = (ctx->sun_skip && env[3] == 0.0f && env[4] >= 0.0f && ctx->hs.colors_finite) ? 1 : 0;
     fp->team = ctx->team;
     fp->max_waves = ctx->max_waves;
     fp->log_buf = nullptr;
@@ -580,6 +583,11 @@ int rt_set_option(rt_ctx* ctx, const char* key, int64_t value) {
         ctx->team = (int)value;
         return RT_OK;
     }
+    if (!std::strcmp(key, "sun_skip")) {
+        if (value != 0 && value != 1) return set_err(ctx, RT_ERR_ARG, "sun_skip must be 0 or 1");
+        ctx->sun_skip = (int)value;
+        return RT_OK;
+    }
     if (!std::strcmp(key, "step")) {
         if (value < 0 || value > 2) return set_err(ctx, RT_ERR_ARG, "step must be 0 (auto), 1 (item) or 2 (round)");
         ctx->step = (int)value;
@@ -625,8 +633,10 @@ int rt_set_scene(rt_ctx* ctx, const float* vp, int64_t nvp, const float* vn, int
     hs.nmat = (int32_t)M;
     hs.nbvh9 = (int32_t)NB;
     hs.mat.assign((size_t)rt::kMatF * M, 0.0f);   // rows padded to kMatF floats (DevScene::mat)
-    for (int64_t m = 0; m < M; ++m)
+    for (int64_t m = 0; m < M; ++m) {
         for (int k = 0; k < 6; ++k) hs.mat[(size_t)rt::kMatF * m + k] = mat[6 * m + k];
+        for (int k = 1; k < 4; ++k) hs.colors_finite = hs.colors_finite && std::isfinite(mat[6 * m + k]);
+    }
     if (bvh9) hs.bvh9.assign(bvh9, bvh9 + nbvh);
     hs.tri_geo.assign((size_t)T * 12, 0.0f);
     hs.tri_shade.assign((size_t)T * 4, 0.0f);
@@ -963,6 +973,7 @@ int rt_debug_pixel_log(rt_ctx* ctx, int traversal, const float cam[10], const fl
     if (!log || cap <= 0 || !n_events || !out3) return set_err(ctx, RT_ERR_ARG, "bad log buffer");
     if (traversal == RT_TRAVERSAL_FAST && !ctx->hs.fast_ok) traversal = RT_TRAVERSAL_REF;
     fp.max_bounce = max_bounce;
+    fp.sun_skip = 0;   // the event log records every ray the reference traces
     Device& d = ctx->devs[0];
     HIP_OR_RET(ctx, hipSetDevice(d.id));
     const size_t obytes = (size_t)fp.nloc * 3 * sizeof(float);

@@ -84,6 +84,10 @@ struct FrameParams {
     int32_t team;        // brute-force path: lanes per pixel (1, 2, 4, 8; 0 = chosen at launch from the tile size)
     int32_t max_waves;   // persistent grid: at most this many waves per SIMD (0 = as many as stay resident)
     int32_t step;        // FAST tree walk: 1 = one item per traversal step, 2 = descend-until-leaf rounds, 0 = auto
+    // FAST: skip the shadow ray when its result cannot change the sample: envData[3] (sun power) == 0,
+    // envData[4] >= 0 and every material colour finite make the sun term of Raytracing.cl:125-137
+    // exactly zero whatever the ray hits (set by the host, never for debug logs)
+    int32_t sun_skip;
     // debug event log of one pixel (rt_debug_pixel_log only; unused by the product launches)
     int64_t log_pixel;
     float* log_buf;

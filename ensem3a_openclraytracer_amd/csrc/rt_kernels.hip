@@ -1116,6 +1116,7 @@ __global__ void RT_RENDER_BOUNDS render_kernel(DevScene S, FrameParams F, float*
             const int hm = h.tri >= 0 ? __float_as_int(tshade[h.tri].w) : 0;
             log_event(F, phase == BOUNCE ? 1.0f : 2.0f, j, Bo, td, h.tri >= 0 ? h.k : -1.0f, hm, so);
         }
+        int sun_hit = -2;   // the shadow ray's hit for the sun term below (-1 = miss; -2 = no sun term now)
         if (phase == BOUNCE) {
             if (h.tri >= 0) {
                 Ro = Bo; Rd = Bd; tri = h.tri; k = h.k;
@@ -1132,15 +1133,20 @@ __global__ void RT_RENDER_BOUNDS render_kernel(DevScene S, FrameParams F, float*
                     so = rtm_scale(so, bm.rough);
                     finish = true;
                 }
+            } else if (TRAV == TRAV_FAST && F.sun_skip) {
+                sun_hit = -1;   // unlit sun: the shadow ray cannot change the sample (FrameParams::sun_skip)
             } else {
                 phase = SUN;
             }
-        } else {  // SUN (Raytracing.cl:115-137)
+        } else {
+            sun_hit = h.tri;
+        }
+        if (sun_hit != -2) {  // SUN (Raytracing.cl:115-137)
             rtm_f3 sunLight = rtm_v3(0, 0, 0);
             const Mat cm = load_mat(tmat, __float_as_int(tshade[tri].w));
-            if (h.tri < 0 && cm.type != 3) sunLight = rtm_v3(e3, e3, e3);
-            if (h.tri >= 0) {
-                const Mat sm = load_mat(tmat, __float_as_int(tshade[h.tri].w));
+            if (sun_hit < 0 && cm.type != 3) sunLight = rtm_v3(e3, e3, e3);
+            if (sun_hit >= 0) {
+                const Mat sm = load_mat(tmat, __float_as_int(tshade[sun_hit].w));
                 if (sm.type == 3) sunLight = rtm_scale(sm.color, e3);
             }
             const rtm_f3 envLight = rtm_scale(sample_ibl_if<COUNT>(S, C, Bd, e4, c), e4);
@@ -1453,10 +1459,15 @@ __global__ void RT_RESUME_BOUNDS render_resume_kernel(DevScene S, FrameParams F,
                     }
                 } else {
                     phase = SUN;   // escaped: shadow ray towards the sun (Raytracing.cl:115-124)
-                    start(Bo, C.sun);
-                    if (!tracing) continue;  // unreachable in practice (root box always hit from inside)
+                    // unlit sun (FrameParams::sun_skip): the shadow ray cannot change the sample; it is not
+                    // traced and the sun term below runs now with h, the bounce ray's miss
+                    if (!F.sun_skip) {
+                        start(Bo, C.sun);
+                        if (!tracing) continue;  // unreachable in practice (root box always hit from inside)
+                    }
                 }
-            } else if (phase == SUN) {  // Raytracing.cl:125-137
+            }
+            if (phase == SUN && !tracing) {  // Raytracing.cl:125-137
                 if (LOG && logme) {
                     const int hm = h.tri >= 0 ? __float_as_int(S.tri_shade[h.tri].w) : 0;
                     log_event(F, 2.0f, j, Bo, C.sun, h.tri >= 0 ? h.k : -1.0f, hm, so);

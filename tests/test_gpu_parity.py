@@ -80,7 +80,11 @@ def test_work_counters_match_oracle(kl, traversal):
     sc, cam, env, npix, spp, mb, ibl = W.PARITY_CASES["monkey_c3_64_s4"].inputs()
     _launch(kl, sc, cam, env, npix, spp, mb, ibl, traversal)
     _, oc = O.render(O.OracleScene.from_scene(sc, ibl), cam, env, npix, spp, mb, nthreads=16, counts=True)
-    gc = kl.native.count_work(cam, env, npix, spp, mb)
+    kl.native.set_option("sun_skip", 0)   # count every ray the reference traces (this case's sun is unlit)
+    try:
+        gc = kl.native.count_work(cam, env, npix, spp, mb)
+    finally:
+        kl.native.set_option("sun_skip", 1)
     assert gc["rays"] == oc["rays"] and gc["env_lookups"] == oc["env"]
     if traversal == "ref":
         assert gc["node_fetches"] == oc["nodes"] and gc["tri_tests"] == oc["tris"]
@@ -220,6 +224,30 @@ def test_resumable_traversal_matches_plain_walk(kl, case):
         np.testing.assert_array_equal(frames[0], f)
     with pytest.raises(_native.NativeError, match="resume_min"):
         kl.native.set_option("resume_min", 65)
+
+
+@pytest.mark.parametrize("case", ["monkey_c3_64_s4", "cornell_64_s4", "serre_96x54_s4"])
+def test_unlit_sun_skips_shadow_rays_without_changing_the_frame(kl, case):
+    """envData[3] == 0 (C3's sun): the shadow ray's hit cannot change the sun term, so FAST does not
+    trace it -- same frame, fewer rays; with the sun lit nothing is skipped."""
+    sc, cam, env, npix, spp, mb, ibl = W.PARITY_CASES[case].inputs()
+    res = {}
+    for env3 in (0.0, 0.7):
+        e = np.array(env, np.float32).copy()
+        e[3] = env3
+        for skip in (1, 0):
+            kl.native.set_option("sun_skip", skip)
+            try:
+                frame = _launch(kl, sc, cam, e, npix, spp, mb, ibl, "fast")
+                rays = kl.native.count_work(cam, e, npix, spp, mb)["rays"]
+            finally:
+                kl.native.set_option("sun_skip", 1)
+            res[env3, skip] = (frame, rays)
+        np.testing.assert_array_equal(res[env3, 1][0], res[env3, 0][0])
+    assert res[0.0, 1][1] < res[0.0, 0][1]
+    assert res[0.7, 1][1] == res[0.7, 0][1]
+    np.testing.assert_array_equal(res[0.0, 1][0], _oracle(sc, cam, np.array([*env[:3], 0.0, env[4]], np.float32),
+                                                          npix, spp, mb, ibl))
 
 
 @pytest.mark.parametrize("case", ["monkey_c3_64_s4", "serre_96x54_s4", "proto_64_s4", "furnace_64_s4"])
