@@ -66,6 +66,7 @@ struct HostScene {
     float root_box[6] = {0, 0, 0, 0, 0, 0};
     bool fast_ok = false;
     bool colors_finite = true;     // every material colour finite (FrameParams::sun_skip)
+    bool has_glass = false;        // some material has type 3 (FrameParams::sun_any)
 };
 
 }  // namespace
@@ -84,6 +85,7 @@ struct rt_ctx {
     int max_waves = 0;  // persistent grid cap in waves per SIMD, 0 = occupancy limit
     int step = 0;       // tree-walk traversal loop: 0 auto, 1 one item per step, 2 descend-until-leaf rounds
     int sun_skip = 1;   // FAST: do not trace shadow rays of an unlit sun (FrameParams::sun_skip)
+    int sun_any = 1;    // FAST tree walk: shadow rays end at their first hit when no material is glass
     int block = 128;
     std::string err;
 };
@@ -471,6 +473,7 @@ int check_frame(rt_ctx* ctx, const float* cam, const float* env, int64_t npix, i
     fp->resume_min = ctx->resume_min;
     fp->step = ctx->step;
     fp->sun_skip = (ctx->sun_skip && env[3] == 0.0f && env[4] >= 0.0f && ctx->hs.colors_finite) ? 1 : 0;
+    fp->sun_any = (ctx->sun_any && !ctx->hs.has_glass) ? 1 : 0;
     fp->team = ctx->team;
     fp->max_waves = ctx->max_waves;
     fp->log_buf = nullptr;
@@ -583,6 +586,11 @@ int rt_set_option(rt_ctx* ctx, const char* key, int64_t value) {
         ctx->team = (int)value;
         return RT_OK;
     }
+    if (!std::strcmp(key, "sun_any")) {
+        if (value != 0 && value != 1) return set_err(ctx, RT_ERR_ARG, "sun_any must be 0 or 1");
+        ctx->sun_any = (int)value;
+        return RT_OK;
+    }
     if (!std::strcmp(key, "sun_skip")) {
         if (value != 0 && value != 1) return set_err(ctx, RT_ERR_ARG, "sun_skip must be 0 or 1");
         ctx->sun_skip = (int)value;
@@ -636,6 +644,7 @@ int rt_set_scene(rt_ctx* ctx, const float* vp, int64_t nvp, const float* vn, int
     for (int64_t m = 0; m < M; ++m) {
         for (int k = 0; k < 6; ++k) hs.mat[(size_t)rt::kMatF * m + k] = mat[6 * m + k];
         for (int k = 1; k < 4; ++k) hs.colors_finite = hs.colors_finite && std::isfinite(mat[6 * m + k]);
+        hs.has_glass = hs.has_glass || (int)mat[6 * m] == 3;
     }
     if (bvh9) hs.bvh9.assign(bvh9, bvh9 + nbvh);
     hs.tri_geo.assign((size_t)T * 12, 0.0f);
@@ -973,7 +982,8 @@ int rt_debug_pixel_log(rt_ctx* ctx, int traversal, const float cam[10], const fl
     if (!log || cap <= 0 || !n_events || !out3) return set_err(ctx, RT_ERR_ARG, "bad log buffer");
     if (traversal == RT_TRAVERSAL_FAST && !ctx->hs.fast_ok) traversal = RT_TRAVERSAL_REF;
     fp.max_bounce = max_bounce;
-    fp.sun_skip = 0;   // the event log records every ray the reference traces
+    fp.sun_skip = 0;   // the event log records every ray the reference traces, with its closest hit
+    fp.sun_any = 0;
     Device& d = ctx->devs[0];
     HIP_OR_RET(ctx, hipSetDevice(d.id));
     const size_t obytes = (size_t)fp.nloc * 3 * sizeof(float);

@@ -88,6 +88,9 @@ struct FrameParams {
     // envData[4] >= 0 and every material colour finite make the sun term of Raytracing.cl:125-137
     // exactly zero whatever the ray hits (set by the host, never for debug logs)
     int32_t sun_skip;
+    // FAST tree walk: with no glass material the sun term depends only on whether the shadow ray hits
+    // anything (Raytracing.cl:125-137), so its traversal ends at the first accepted triangle
+    int32_t sun_any;
     // debug event log of one pixel (rt_debug_pixel_log only; unused by the product launches)
     int64_t log_pixel;
     float* log_buf;

@@ -1194,6 +1194,7 @@ struct FastRay {
     float bk;         // best distance
     int bt;           // best triangle's byte offset (48 t), -1 = none
     int brank;        // its rank in the reference DFS order
+    bool any;         // any hit ends the ray (a shadow ray whose hit only matters as hit / miss)
 };
 
 // Returns true when the ray is already finished (no triangles / root box missed).
@@ -1241,6 +1242,7 @@ __device__ __forceinline__ bool fast_round(const DevScene& S, FastRay& R, const 
             R.bk = k;
             R.bt = (int)toff;
             R.brank = rank;
+            if (R.any) return true;
         }
     }
     while (R.soff > 0) {   // pop the next item still in front of the best hit
@@ -1287,6 +1289,7 @@ __device__ __forceinline__ bool fast_step(const DevScene& S, FastRay& R, const c
             R.bk = k;
             R.bt = (int)~(unsigned)R.item;
             R.brank = rank;
+            if (R.any) return true;
         }
     }
     while (R.soff > 0) {   // pop the next item still in front of the best hit
@@ -1356,7 +1359,7 @@ __global__ void RT_RESUME_BOUNDS render_resume_kernel(DevScene S, FrameParams F,
     bool tracing = false;
     PixelQueue pq;
     FastRay T;
-    T.item = 0; T.soff = 0; T.bk = 1000.0f; T.bt = -1; T.brank = -1;
+    T.item = 0; T.soff = 0; T.bk = 1000.0f; T.bt = -1; T.brank = -1; T.any = false;
     T.o = rtm_v3(0, 0, 0); T.d = rtm_v3(0, 0, 1); T.ix = T.iy = T.iz = 0.0f;
     int p = 0, i = 0;
     bool logme = false;
@@ -1388,6 +1391,7 @@ __global__ void RT_RESUME_BOUNDS render_resume_kernel(DevScene S, FrameParams F,
     };
     auto start = [&](rtm_f3 o, rtm_f3 d) __attribute__((always_inline)) {
         tracing = !fast_init<COUNT>(S, T, o, d, c);
+        T.any = false;
     };
 
     while (true) {
@@ -1463,6 +1467,7 @@ __global__ void RT_RESUME_BOUNDS render_resume_kernel(DevScene S, FrameParams F,
                     // traced and the sun term below runs now with h, the bounce ray's miss
                     if (!F.sun_skip) {
                         start(Bo, C.sun);
+                        T.any = F.sun_any != 0;
                         if (!tracing) continue;  // unreachable in practice (root box always hit from inside)
                     }
                 }

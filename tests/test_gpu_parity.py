@@ -250,6 +250,30 @@ def test_unlit_sun_skips_shadow_rays_without_changing_the_frame(kl, case):
                                                           npix, spp, mb, ibl))
 
 
+@pytest.mark.parametrize("case", ["grid", "cornell_64_s4"])
+def test_shadow_rays_end_at_first_hit_without_glass(kl, case):
+    """No glass material: the sun term only asks whether the shadow ray hits anything, so the tree walk
+    stops at the first accepted triangle (sun_any) -- same frame as the closest-hit walk, fewer nodes."""
+    if case == "grid":
+        sc, cam, env, npix, spp, mb, ibl = W.CONFIGS["C5"].with_size(48, 27, 2).inputs()
+    else:
+        sc, cam, env, npix, spp, mb, ibl = W.PARITY_CASES[case].inputs()
+    assert not (sc.materialData.reshape(-1, 6)[:, 0].astype(int) == 3).any() and env[3] != 0
+    frames, nodes = [], []
+    kl.native.set_option("brute_max", 0)   # the tree walk
+    try:
+        for any_hit in (1, 0):
+            kl.native.set_option("sun_any", any_hit)
+            frames.append(_launch(kl, sc, cam, env, npix, spp, mb, ibl, "fast"))
+            nodes.append(kl.native.count_work(cam, env, npix, spp, mb)["node_fetches"])
+    finally:
+        kl.native.set_option("sun_any", 1)
+        kl.native.set_option("brute_max", 64)
+    np.testing.assert_array_equal(frames[0], frames[1])
+    np.testing.assert_array_equal(frames[0], _oracle(sc, cam, env, npix, spp, mb, ibl))
+    assert nodes[0] < nodes[1]
+
+
 @pytest.mark.parametrize("case", ["monkey_c3_64_s4", "serre_96x54_s4", "proto_64_s4", "furnace_64_s4"])
 def test_traversal_step_modes_render_identically(kl, case):
     """step: one node-or-leaf item per traversal step (same four loads for both) or descend-until-leaf
