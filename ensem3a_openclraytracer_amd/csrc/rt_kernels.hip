@@ -1619,15 +1619,17 @@ hipError_t launch_t(const DevScene& sc, const FrameParams& fp, int block, float*
     const int cap_cu = fp.max_waves > 0 ? std::max(1, fp.max_waves * 4 * 64 / block) : INT_MAX;
     const int64_t resident = (int64_t)std::max(1, cus) * std::max(1, std::min(per_cu, cap_cu));
     // brute-force teams: a tile with fewer pixels than the device has lanes (a row slice of a
-    // multi-GPU frame) gives each pixel 2 or 4 lanes that split its box tests
+    // multi-GPU frame) gives each pixel 4 lanes that split its box tests when it fills at most a quarter of them
     FrameParams f = fp;
     f.team = 1;
     if (BRUTE) {
         f.team = fp.team;
         if (f.team == 0) {
+            // measured on C2 tiles (one MI355X, 96-VGPR kernel: 327,680 resident lanes): a 1/8 tile
+            // (131k pixels) is fastest with single lanes (2.23 vs 2.29 ms with pairs), a 1/16 tile with
+            // teams of 4 (1.67 vs 1.88 with pairs, 2.28 single)
             const int64_t lanes = resident * block;
-            f.team = 1;
-            while (f.team < 4 && fp.nloc * (f.team * 2) <= lanes) f.team *= 2;
+            f.team = fp.nloc * 4 <= lanes ? 4 : 1;
         }
     }
     const int64_t need = (fp.nloc * f.team + block - 1) / block;
