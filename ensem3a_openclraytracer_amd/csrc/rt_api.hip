@@ -28,6 +28,12 @@
 #ifndef RT_RESUME_MIN_DEFAULT
 #define RT_RESUME_MIN_DEFAULT 40  // FAST tree walk: resumable traversal threshold (rt_set_option "resume_min")
 #endif
+#ifndef RT_COMPACT_DEFAULT
+#define RT_COMPACT_DEFAULT 0   // option "compact"
+#endif
+#ifndef RT_NODE_ORDER
+#define RT_NODE_ORDER 0        // FAST node numbering: 0 breadth-first, 1 depth-first preorder
+#endif
 #ifndef RT_BRUTE_MAX_DEFAULT
 #define RT_BRUTE_MAX_DEFAULT 64   // FAST tests every triangle of scenes up to this size (rt_set_option "brute_max")
 #endif
@@ -46,7 +52,7 @@ struct Device {
     hipStream_t stream = nullptr;
     int cus = 0;                  // compute units (sizes the FAST stack overflow buffer)
     DevBuf stack_ovf;             // FAST traversal stack entries beyond the LDS part
-    DevBuf nodes, brute, brute_box, bvh9, tri_geo, tri_shade, tri_frame, mat, ibl, out, out8, counts, work, scratch_a, scratch_b;
+    DevBuf nodes, nodes48, tri2, brute, brute_box, bvh9, tri_geo, tri_shade, tri_frame, mat, ibl, out, out8, counts, work, scratch_a, scratch_b;
     char* host_stage = nullptr;   // pinned staging for rt_render / rt_render_rgb8
     size_t host_stage_bytes = 0;
 };
@@ -54,6 +60,9 @@ struct Device {
 // Host copy of the packed scene (kept to upload on every device).
 struct HostScene {
     std::vector<float> nodes;      // 16 floats per internal node
+    std::vector<float> nodes48;    // 12 floats per internal node, child refs in the box bits (DevScene::nodes48)
+    std::vector<float> tri2;       // 24 floats per internal node: its leaf children's records (DevScene::tri2)
+    int32_t root_ref48 = 0;
     std::vector<float> bvh9;
     std::vector<float> tri_geo;    // 12 floats per triangle
     std::vector<float> tri_shade;  // 4 floats per triangle
@@ -86,6 +95,7 @@ struct rt_ctx {
     int step = 0;       // tree-walk traversal loop: 0 auto, 1 one item per step, 2 descend-until-leaf rounds
     int sun_skip = 1;   // FAST: do not trace shadow rays of an unlit sun (FrameParams::sun_skip)
     int sun_any = 1;    // FAST tree walk: shadow rays end at their first hit when no material is glass
+    int compact = RT_COMPACT_DEFAULT;   // item-step tree walk on the compact node layout (DevScene::nodes48)
     int block = 128;
     std::string err;
 };
@@ -151,6 +161,23 @@ inline bool fidx(float v, int64_t limit, int32_t* out) {
     return true;
 }
 
+// Move v outwards (down for a lower bound, up for an upper bound) to the nearest float whose low 4
+// bits are nib.  False if no finite such float is close.
+bool embed_nibble(float& v, uint32_t nib, bool lower) {
+    float f = v;
+    for (int i = 0; i < 64; ++i) {
+        if (!std::isfinite(f)) return false;
+        uint32_t b;
+        std::memcpy(&b, &f, 4);
+        if ((b & 15u) == nib) {
+            v = f;
+            return true;
+        }
+        f = std::nextafter(f, lower ? -INFINITY : INFINITY);
+    }
+    return false;
+}
+
 // Emit the FAST node array from a binary tree with one triangle per leaf:
 // internal nodes in BFS order, each holding its children's boxes and refs.
 // box: 6 floats per tree node (lo.xyz, hi.xyz).
@@ -182,6 +209,22 @@ void emit_bvh(HostScene& hs, const int32_t* L, const int32_t* R, const int32_t* 
     };
     std::vector<int32_t> wide_of(nn, -1), bfs;
     std::vector<std::vector<int32_t>> children;
+#if RT_NODE_ORDER == 1
+    // depth-first preorder: every subtree's nodes are contiguous
+    if (is_inner(0)) {
+        std::vector<int32_t> st{0};
+        while (!st.empty()) {
+            const int32_t n = st.back();
+            st.pop_back();
+            wide_of[n] = (int32_t)bfs.size();
+            bfs.push_back(n);
+            children.push_back(kids(n));
+            const std::vector<int32_t>& k = children.back();
+            for (int i = (int)k.size() - 1; i >= 0; --i)
+                if (is_inner(k[i])) st.push_back(k[i]);
+        }
+    }
+#else
     if (is_inner(0)) {
         bfs.push_back(0);
         wide_of[0] = 0;
@@ -194,6 +237,7 @@ void emit_bvh(HostScene& hs, const int32_t* L, const int32_t* R, const int32_t* 
             bfs.push_back(ch);
         }
     }
+#endif
     // stack bound: a node pushes (children - 1) entries at most; need = max over root-to-leaf
     // paths of the sum (children are after their parents in BFS order: sweep backwards)
     std::vector<int32_t> need(bfs.size(), 0);
@@ -231,6 +275,46 @@ void emit_bvh(HostScene& hs, const int32_t* L, const int32_t* R, const int32_t* 
         }
     }
     hs.root_ref = is_inner(0) ? 0 : ~(48 * T[0]);
+    // compact item layout of the item-step tree walk (rt_internal.h DevScene::nodes48 / tri2): a node
+    // is its 48 bytes of child boxes; the ref of an internal child ((BFS index << 2) | its child-is-leaf
+    // bits) is written into the low 4 bits of that child's six box coordinates, each moved outwards
+    // to the nearest float with the wanted bits (an internal box only prunes, a larger one prunes
+    // less: same hits); leaf boxes stay exact and a leaf child's triangle record sits at slot 2 w + c
+    hs.nodes48.clear();
+    hs.tri2.clear();
+    hs.root_ref48 = 0;
+    if (W == 2 && is_inner(0) && bfs.size() < (size_t)1 << 22) {
+        auto types = [&](size_t w) {
+            return (uint32_t)(is_inner(children[w][0]) ? 0 : 1) | (uint32_t)(is_inner(children[w][1]) ? 0 : 2);
+        };
+        bool ok = true;
+        constexpr size_t CS = rt::kCompactStride / 4;   // floats per record
+        hs.nodes48.assign(bfs.size() * CS, 0.0f);
+        hs.tri2.assign(bfs.size() * 2 * CS, 0.0f);
+        for (size_t w = 0; w < bfs.size() && ok; ++w) {
+            float* q = hs.nodes48.data() + CS * w;
+            for (int k = 0; k < 12; ++k) q[k] = hs.nodes[(size_t)F * w + k];
+            for (int c = 0; c < 2 && ok; ++c) {
+                const int32_t ch = children[w][c];
+                if (is_inner(ch)) {
+                    const uint32_t r = ((uint32_t)wide_of[ch] << 2) | types((size_t)wide_of[ch]);
+                    // the child's lo.x hi.x lo.y hi.y lo.z hi.z in the node
+                    const int at[6] = {4 * c, 4 * c + 1, 4 * c + 2, 4 * c + 3, 8 + 2 * c, 9 + 2 * c};
+                    for (int k = 0; k < 6 && ok; ++k) ok = embed_nibble(q[at[k]], (r >> (4 * k)) & 15u, (k & 1) == 0);
+                } else {
+                    float* t2 = hs.tri2.data() + CS * (2 * w + c);
+                    for (int k = 0; k < 12; ++k) t2[k] = hs.tri_geo[12 * (size_t)T[ch] + k];
+                    t2[7] = as_f32(T[ch]);   // e1.w: the triangle index
+                }
+            }
+        }
+        if (ok) {
+            hs.root_ref48 = (int32_t)types(0);
+        } else {
+            hs.nodes48.clear();
+            hs.tri2.clear();
+        }
+    }
     for (int k = 0; k < 6; ++k) hs.root_box[k] = box[k];
     hs.depth = bfs.empty() ? 1 : std::max(1, need[0]);
 }
@@ -426,6 +510,9 @@ hipError_t upload(DevBuf& b, const std::vector<T>& v, hipStream_t s) {
 rt::DevScene dev_scene(const rt_ctx* ctx, const Device& d) {
     rt::DevScene s{};
     s.nodes = (const float4*)d.nodes.p;
+    s.nodes48 = ctx->hs.nodes48.empty() ? nullptr : (const float4*)d.nodes48.p;
+    s.tri2 = ctx->hs.tri2.empty() ? nullptr : (const float4*)d.tri2.p;
+    s.root_ref48 = ctx->hs.root_ref48;
     s.nnodes = ctx->hs.nnodes;
     s.root_ref = ctx->hs.root_ref;
     for (int k = 0; k < 6; ++k) s.root_box[k] = ctx->hs.root_box[k];
@@ -474,6 +561,7 @@ int check_frame(rt_ctx* ctx, const float* cam, const float* env, int64_t npix, i
     fp->step = ctx->step;
     fp->sun_skip = (ctx->sun_skip && env[3] == 0.0f && env[4] >= 0.0f && ctx->hs.colors_finite) ? 1 : 0;
     fp->sun_any = (ctx->sun_any && !ctx->hs.has_glass) ? 1 : 0;
+    fp->compact = ctx->compact;
     fp->team = ctx->team;
     fp->max_waves = ctx->max_waves;
     fp->log_buf = nullptr;
@@ -531,7 +619,7 @@ void rt_destroy(rt_ctx* ctx) {
     for (auto& d : ctx->devs) {
         if (hipSetDevice(d.id) != hipSuccess) continue;
         if (d.stream) (void)hipStreamSynchronize(d.stream);
-        for (DevBuf* b : {&d.stack_ovf, &d.nodes, &d.brute, &d.brute_box, &d.bvh9, &d.tri_geo, &d.tri_shade, &d.tri_frame, &d.mat, &d.ibl, &d.out,
+        for (DevBuf* b : {&d.stack_ovf, &d.nodes, &d.nodes48, &d.tri2, &d.brute, &d.brute_box, &d.bvh9, &d.tri_geo, &d.tri_shade, &d.tri_frame, &d.mat, &d.ibl, &d.out,
                           &d.counts, &d.work, &d.scratch_a, &d.scratch_b})
             release(*b);
         if (d.host_stage) (void)hipHostFree(d.host_stage);
@@ -566,6 +654,8 @@ int rt_set_option(rt_ctx* ctx, const char* key, int64_t value) {
         for (auto& d : ctx->devs) {
             HIP_OR_RET(ctx, hipSetDevice(d.id));
             HIP_OR_RET(ctx, upload(d.nodes, hs.nodes, d.stream));
+            HIP_OR_RET(ctx, upload(d.nodes48, hs.nodes48, d.stream));
+            HIP_OR_RET(ctx, upload(d.tri2, hs.tri2, d.stream));
             HIP_OR_RET(ctx, upload(d.brute, hs.brute, d.stream));
             HIP_OR_RET(ctx, upload(d.brute_box, hs.brute_box, d.stream));
             HIP_OR_RET(ctx, upload(d.tri_geo, hs.tri_geo, d.stream));
@@ -584,6 +674,11 @@ int rt_set_option(rt_ctx* ctx, const char* key, int64_t value) {
         if (value != 0 && value != 1 && value != 2 && value != 4 && value != 8)
             return set_err(ctx, RT_ERR_ARG, "team must be 0 (auto), 1, 2, 4 or 8");
         ctx->team = (int)value;
+        return RT_OK;
+    }
+    if (!std::strcmp(key, "compact")) {
+        if (value != 0 && value != 1) return set_err(ctx, RT_ERR_ARG, "compact must be 0 or 1");
+        ctx->compact = (int)value;
         return RT_OK;
     }
     if (!std::strcmp(key, "sun_any")) {
@@ -702,6 +797,8 @@ int rt_set_scene(rt_ctx* ctx, const float* vp, int64_t nvp, const float* vn, int
     for (auto& d : ctx->devs) {
         HIP_OR_RET(ctx, hipSetDevice(d.id));
         HIP_OR_RET(ctx, upload(d.nodes, hs.nodes, d.stream));
+        HIP_OR_RET(ctx, upload(d.nodes48, hs.nodes48, d.stream));
+        HIP_OR_RET(ctx, upload(d.tri2, hs.tri2, d.stream));
         HIP_OR_RET(ctx, upload(d.brute, hs.brute, d.stream));
         HIP_OR_RET(ctx, upload(d.brute_box, hs.brute_box, d.stream));
         HIP_OR_RET(ctx, ensure_stack_ovf(d, hs));

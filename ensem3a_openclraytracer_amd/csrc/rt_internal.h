@@ -23,6 +23,12 @@ constexpr int kMaxLanesPerCu = 2048;   // resident threads per CU (gfx950)
 #endif
 constexpr int kBoxGroup = RT_BOX_GROUP;
 constexpr int kMatF = 8;   // floats per device material row (DevScene::mat)
+// bytes per node / per triangle record of the compact item layout (DevScene::nodes48, tri2): 48 B of
+// data each, 64 keeps them aligned to cache sectors
+#ifndef RT_COMPACT_STRIDE
+#define RT_COMPACT_STRIDE 64
+#endif
+constexpr int kCompactStride = RT_COMPACT_STRIDE;
 // brute-force records whose leaf boxes are bit-identical share one box test (DevScene::brute_box)
 #ifndef RT_BOX_DEDUP
 #define RT_BOX_DEDUP 1
@@ -37,6 +43,14 @@ struct DevScene {
     //   [3] = child refs (int bits): >= 0 internal node, < 0 leaf = ~(48 * triangle), its tri_geo byte offset
     const float4* nodes;
     int32_t nnodes;        // internal nodes in `nodes`
+    // the same tree for the item-step walk, 3 x float4 per node (nullptr: not built): the first three
+    // float4 of `nodes`, where each internal child's six coordinates carry 4 bits of its ref in their
+    // low bits (moved outwards: a slightly larger box).  Refs: (BFS index << 2) | bit c set when child
+    // c is a leaf; a leaf child's ref is ~(48 * (2 * index + c)), the byte offset of its record in tri2
+    // (tri_geo's record with e1.w = the triangle index)
+    const float4* nodes48;
+    const float4* tri2;
+    int32_t root_ref48;
     int32_t root_ref;      // ref of the root (~(48 * tri) when the root is a leaf)
     float root_box[6];     // min.xyz, max.xyz of the root
     // REF traversal: the reference's own AoS export, 9 floats per node
@@ -91,6 +105,7 @@ struct FrameParams {
     // FAST tree walk: with no glass material the sun term depends only on whether the shadow ray hits
     // anything (Raytracing.cl:125-137), so its traversal ends at the first accepted triangle
     int32_t sun_any;
+    int32_t compact;     // item-step tree walk: use DevScene::nodes48 when built
     // debug event log of one pixel (rt_debug_pixel_log only; unused by the product launches)
     int64_t log_pixel;
     float* log_buf;

@@ -1264,20 +1264,36 @@ __device__ __forceinline__ bool fast_round(const DevScene& S, FastRay& R, const 
 // with all its tracing lanes active.  On C3 the texture address unit was 89 % busy with the
 // descend-until-leaf rounds of fast_round, whose loads ran with few lanes active.
 // Returns true when the ray is finished.
-template <bool COUNT, bool SOA, bool OVF>
+// 4 low bits of each of six floats -> a 24-bit child ref (DevScene::nodes48)
+__device__ __forceinline__ int nib6(float a, float b, float c, float d, float e, float f) {
+    return (int)((__float_as_uint(a) & 15u) | ((__float_as_uint(b) & 15u) << 4) | ((__float_as_uint(c) & 15u) << 8) |
+                 ((__float_as_uint(d) & 15u) << 12) | ((__float_as_uint(e) & 15u) << 16) |
+                 ((__float_as_uint(f) & 15u) << 20));
+}
+
+// COMPACT: nb / tb are DevScene::nodes48 / tri2 -- a node is 48 bytes, so an item takes three loads.
+template <bool COUNT, bool SOA, bool OVF, bool COMPACT = false>
 __device__ __forceinline__ bool fast_step(const DevScene& S, FastRay& R, const char* nb, const char* tb,
                                           const LaneStack& st, unsigned kstride, Cnt& c) {
 #if RT_BVH_WIDTH != 4
     const bool node = R.item >= 0;
-    const char* p = node ? nb + (SOA ? 16u : 16u * kNodeF4) * (unsigned)R.item : tb + ~(unsigned)R.item;
-    const unsigned ks = node ? kstride : 16u;
+    const char* p = COMPACT ? (node ? nb + (unsigned)kCompactStride * ((unsigned)R.item >> 2) : tb + ~(unsigned)R.item)
+                            : (node ? nb + (SOA ? 16u : 16u * kNodeF4) * (unsigned)R.item : tb + ~(unsigned)R.item);
+    const unsigned ks = (COMPACT || !node) ? 16u : kstride;
     const float4 g0 = *reinterpret_cast<const float4*>(p);
     const float4 g1 = *reinterpret_cast<const float4*>(p + ks);
     const float4 g2 = *reinterpret_cast<const float4*>(p + 2 * ks);
-    const int2 e = *reinterpret_cast<const int2*>(p + (node ? 3 * ks : 0u));
+    int2 e = make_int2(0, 0);
+    if (!COMPACT) e = *reinterpret_cast<const int2*>(p + (node ? 3 * ks : 0u));
     if (COUNT) count_wave(c.wave_trav);
     if (node) {
         if (COUNT) c.nodes++;
+        if (COMPACT) {
+            const unsigned x = (unsigned)R.item >> 2, ty = (unsigned)R.item & 3u;
+            constexpr unsigned cs = (unsigned)kCompactStride;
+            e.x = (ty & 1u) ? (int)~(2u * cs * x) : nib6(g0.x, g0.y, g0.z, g0.w, g2.x, g2.y);
+            e.y = (ty & 2u) ? (int)~(2u * cs * x + cs) : nib6(g1.x, g1.y, g1.z, g1.w, g2.z, g2.w);
+        }
         const float oix = R.o.x * R.ix, oiy = R.o.y * R.iy, oiz = R.o.z * R.iz;
         R.item = node_pick<OVF>(g0, g1, g2, e, R.o, R.ix, R.iy, R.iz, oix, oiy, oiz, R.bk * CULL_MARGIN, st, R.soff);
         if (R.item != INT_MIN) return false;
@@ -1287,7 +1303,7 @@ __device__ __forceinline__ bool fast_step(const DevScene& S, FastRay& R, const c
         int rank;
         if (mt_vals(g0, g1, g2, R.o, R.d, &k, &rank) && k > 0.0001f && (k < R.bk || (k == R.bk && rank < R.brank))) {
             R.bk = k;
-            R.bt = (int)~(unsigned)R.item;
+            R.bt = COMPACT ? 48 * __float_as_int(g1.w) : (int)~(unsigned)R.item;
             R.brank = rank;
             if (R.any) return true;
         }
@@ -1323,7 +1339,7 @@ __device__ __forceinline__ bool fast_step(const DevScene& S, FastRay& R, const c
 #define RT_RESUME_BOUNDS __launch_bounds__(256)
 #endif
 
-template <bool COUNT, bool LOG, bool SMEM, bool OVF, bool STEP>
+template <bool COUNT, bool LOG, bool SMEM, bool OVF, bool STEP, bool COMPACT>
 __global__ void RT_RESUME_BOUNDS render_resume_kernel(DevScene S, FrameParams F, float* __restrict__ out,
                                                       unsigned long long* __restrict__ counts,
                                                       unsigned int* __restrict__ work_counter,
@@ -1347,6 +1363,8 @@ __global__ void RT_RESUME_BOUNDS render_resume_kernel(DevScene S, FrameParams F,
     const LaneStack lst = lane_stack(S, lds_stack);
     const char* const nb = reinterpret_cast<const char*>(nodes);
     const char* const tb = reinterpret_cast<const char*>(tris);
+    const char* const nb48 = reinterpret_cast<const char*>(S.nodes48);   // COMPACT item steps
+    const char* const tb2 = reinterpret_cast<const char*>(S.tri2);
     const unsigned kstride = SMEM ? 16u * (unsigned)S.nnodes : 16u;
     const int W = F.width;
     const int imgSize = (int)F.npix;
@@ -1391,6 +1409,7 @@ __global__ void RT_RESUME_BOUNDS render_resume_kernel(DevScene S, FrameParams F,
     };
     auto start = [&](rtm_f3 o, rtm_f3 d) __attribute__((always_inline)) {
         tracing = !fast_init<COUNT>(S, T, o, d, c);
+        if (COMPACT) T.item = S.root_ref48;
         T.any = false;
     };
 
@@ -1539,7 +1558,8 @@ __global__ void RT_RESUME_BOUNDS render_resume_kernel(DevScene S, FrameParams F,
             if (lane == 0) c.cyc_shade += t_mid - t_iter;
         }
         while (true) {
-            if (tracing && (STEP ? fast_step<COUNT, SMEM, OVF>(S, T, nb, tb, lst, kstride, c)
+            if (tracing && (STEP ? fast_step<COUNT, SMEM, OVF, COMPACT>(S, T, COMPACT ? nb48 : nb, COMPACT ? tb2 : tb,
+                                                                         lst, kstride, c)
                                  : fast_round<COUNT, SMEM, OVF>(S, T, nb, tb, lst, kstride, c)))
                 tracing = false;
             const unsigned long long tr = __ballot(tracing);
@@ -1594,7 +1614,7 @@ __global__ void rgb8_kernel(const float* __restrict__ in, uint8_t* __restrict__ 
 }
 
 template <int TRAV, bool COUNT, bool LOG, bool SMEM = false, bool RESUME = false, bool OVF = false,
-          bool BRUTE = false, bool STEP = true>
+          bool BRUTE = false, bool STEP = true, bool COMPACT = false>
 hipError_t launch_t(const DevScene& sc, const FrameParams& fp, int block, float* d_out, unsigned long long* d_counts,
                     unsigned int* d_work, hipStream_t stream) {
     // FAST: int2 entries; the brute-force path of small scenes needs no stack
@@ -1611,7 +1631,7 @@ hipError_t launch_t(const DevScene& sc, const FrameParams& fp, int block, float*
     int dev = 0, cus = 0, per_cu = 0;
     hipError_t e = hipGetDevice(&dev);
     if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    const void* kfn = RESUME ? (const void*)render_resume_kernel<COUNT, LOG, SMEM, OVF, STEP>
+    const void* kfn = RESUME ? (const void*)render_resume_kernel<COUNT, LOG, SMEM, OVF, STEP, COMPACT>
                              : (const void*)render_kernel<TRAV, COUNT, LOG, SMEM, OVF, BRUTE ? 1 : 0>;
     if (e == hipSuccess) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kfn, block, lds);
     if (e != hipSuccess) return e;
@@ -1648,7 +1668,7 @@ hipError_t launch_t(const DevScene& sc, const FrameParams& fp, int block, float*
     LaunchConst* lc = reinterpret_cast<LaunchConst*>(reinterpret_cast<char*>(d_work) + 64);
     hipLaunchKernelGGL(make_const_kernel, dim3(1), dim3(64), 0, stream, f, lc);
     if (RESUME)
-        hipLaunchKernelGGL((render_resume_kernel<COUNT, LOG, SMEM, OVF, STEP>), dim3((unsigned)grid), dim3(block), lds, stream,
+        hipLaunchKernelGGL((render_resume_kernel<COUNT, LOG, SMEM, OVF, STEP, COMPACT>), dim3((unsigned)grid), dim3(block), lds, stream,
                            sc, f, d_out, d_counts, d_work, (const LaunchConst*)lc);
     else if (BRUTE && f.team > 1)
         hipLaunchKernelGGL((render_kernel<TRAV, COUNT, LOG, SMEM, OVF, BRUTE ? 2 : 0>), dim3((unsigned)grid),
@@ -1741,6 +1761,14 @@ hipError_t launch_debug_trace(const DevScene& sc, int traversal, const float* ra
 template <bool COUNT, bool STEP>
 hipError_t launch_resume(const DevScene& sc, const FrameParams& fp, int block, float* d_out,
                          unsigned long long* d_counts, unsigned int* d_work, hipStream_t stream, bool smem, bool ovf) {
+    // item steps on the compact 48-byte nodes: three loads per item instead of four
+    if (STEP && !smem && fp.compact && sc.nodes48 && sc.tri2) {
+        if (ovf)
+            return launch_t<TRAV_FAST, COUNT, false, false, true, true, false, true, true>(sc, fp, block, d_out,
+                                                                                         d_counts, d_work, stream);
+        return launch_t<TRAV_FAST, COUNT, false, false, true, false, false, true, true>(sc, fp, block, d_out, d_counts,
+                                                                                      d_work, stream);
+    }
     if (smem)
         return launch_t<TRAV_FAST, COUNT, false, true, true, false, false, STEP>(sc, fp, block, d_out, d_counts,
                                                                                  d_work, stream);
