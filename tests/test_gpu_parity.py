@@ -164,6 +164,47 @@ def test_brute_force_path_matches_tree_walk(kl, case):
     assert brute_counts["node_fetches"] == brute_counts["rays"] * (sc.faceData.size // 10)
 
 
+def test_brute_force_shared_boxes_and_coincident_triangles(kl):
+    """Cornell with a third triangle over every rectangle (three corners of the quad): three records
+    share one leaf box (the box-test dedup groups at most two, so one box is tested twice) and the
+    coplanar triangles hit at equal distances (ties go to the lower reference DFS rank).  Brute force
+    and tree walk give the same frame, bit-identical to the oracle."""
+    import types
+    from ensem3a_openclraytracer_amd import bvh as B
+    wl = W.PARITY_CASES["cornell_64_s4"]
+    sc0, cam, env, npix, spp, mb, ibl = wl.inputs()
+    face = sc0.faceData.reshape(-1, 10)
+    vp = sc0.V_p.reshape(-1, 3)
+    box = lambda f: np.concatenate([vp[f[7:10]].min(0), vp[f[7:10]].max(0)])
+    extra = []
+    for a in range(len(face)):
+        for b in range(a + 1, len(face)):
+            if face[a, 0] != face[b, 0] or not np.array_equal(box(face[a]), box(face[b])):
+                continue
+            pa, pb = list(face[a, 7:10]), list(face[b, 7:10])
+            shared = [v for v in pa if v in pb]
+            if len(set(pa) | set(pb)) != 4 or len(shared) != 2:
+                continue
+            tri = [v for v in pa if v != shared[0]] + [v for v in pb if v not in pa]   # drop one shared corner
+            row = face[a].copy()
+            row[7:10] = tri
+            if np.array_equal(box(row), box(face[a])):
+                extra.append(row)
+    assert len(extra) >= 10
+    fd = np.concatenate([face] + [np.array(extra)]).astype(np.int32).ravel()
+    sc = types.SimpleNamespace(V_p=sc0.V_p, V_n=sc0.V_n, V_uv=sc0.V_uv, faceData=fd, materialData=sc0.materialData,
+                               lightData=sc0.lightData, BVH=B.BVH(fd, sc0.V_p))
+    assert sc.faceData.size // 10 <= 64
+    a = _launch(kl, sc, cam, env, npix, spp, mb, ibl, "fast")
+    kl.native.set_option("brute_max", 0)
+    try:
+        b = _launch(kl, sc, cam, env, npix, spp, mb, ibl, "fast")
+    finally:
+        kl.native.set_option("brute_max", 64)
+    np.testing.assert_array_equal(a, b)
+    np.testing.assert_array_equal(a, _oracle(sc, cam, env, npix, spp, mb, ibl))
+
+
 @pytest.mark.parametrize("case", ["cornell_64_s4", "cornell_64_b0"])
 def test_brute_force_teams_render_identically(kl, case):
     """team = lanes sharing one pixel's box tests (auto for small tiles): the frame and the work
