@@ -23,8 +23,14 @@
 namespace rt {
 namespace {
 
-constexpr int kSweepMax = 64;
-constexpr int kBins = 32;
+#ifndef RT_SAH_SWEEP_MAX
+#define RT_SAH_SWEEP_MAX 64
+#endif
+#ifndef RT_SAH_BINS
+#define RT_SAH_BINS 32
+#endif
+constexpr int kSweepMax = RT_SAH_SWEEP_MAX;
+constexpr int kBins = RT_SAH_BINS;
 
 struct Box {
     float lo[3], hi[3];
