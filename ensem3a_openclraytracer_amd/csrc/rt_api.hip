@@ -28,6 +28,9 @@
 #ifndef RT_RESUME_MIN_DEFAULT
 #define RT_RESUME_MIN_DEFAULT 40  // FAST tree walk: resumable traversal threshold (rt_set_option "resume_min")
 #endif
+#ifndef RT_TRI_ORDER
+#define RT_TRI_ORDER 1         // FAST triangle records: 1 in the tree's depth-first leaf order, 0 reference order
+#endif
 #ifndef RT_COMPACT_DEFAULT
 #define RT_COMPACT_DEFAULT 0   // option "compact"
 #endif
@@ -52,7 +55,7 @@ struct Device {
     hipStream_t stream = nullptr;
     int cus = 0;                  // compute units (sizes the FAST stack overflow buffer)
     DevBuf stack_ovf;             // FAST traversal stack entries beyond the LDS part
-    DevBuf nodes, nodes48, tri2, brute, brute_box, bvh9, tri_geo, tri_shade, tri_frame, mat, ibl, out, out8, counts, work, scratch_a, scratch_b;
+    DevBuf nodes, nodes48, tri2, tri_fast, brute, brute_box, bvh9, tri_geo, tri_shade, tri_frame, mat, ibl, out, out8, counts, work, scratch_a, scratch_b;
     char* host_stage = nullptr;   // pinned staging for rt_render / rt_render_rgb8
     size_t host_stage_bytes = 0;
 };
@@ -65,6 +68,7 @@ struct HostScene {
     int32_t root_ref48 = 0;
     std::vector<float> bvh9;
     std::vector<float> tri_geo;    // 12 floats per triangle
+    std::vector<float> tri_fast;   // tri_geo's records in FAST leaf order (DevScene::tri_fast)
     std::vector<float> tri_shade;  // 4 floats per triangle
     std::vector<float> mat;
     std::vector<float> brute;      // 16 floats per triangle, small scenes only (rt_internal.h DevScene::brute)
@@ -248,12 +252,38 @@ void emit_bvh(HostScene& hs, const int32_t* L, const int32_t* R, const int32_t* 
         need[w] = (int32_t)children[w].size() - 1 + sub;
     }
     constexpr int F = 4 * (W == 4 ? 8 : 4);   // floats per node
+    // the FAST traversal's triangle records (DevScene::tri_fast), in the order a depth-first walk of
+    // this tree meets its leaves (RT_TRI_ORDER 1) or in reference order (0): pos[t] = record of t
+    std::vector<int32_t> pos((size_t)hs.ntri, -1);
+    {
+        int32_t next = 0;
+        auto place = [&](int32_t c) {
+            if (!is_inner(c) && T[c] >= 0 && pos[T[c]] < 0) pos[T[c]] = next++;
+        };
+        if (RT_TRI_ORDER == 1 && is_inner(0)) {
+            std::vector<int32_t> st{0};
+            while (!st.empty()) {
+                const int32_t w = st.back();
+                st.pop_back();
+                const auto& k = children[w];
+                for (int32_t c : k) place(c);
+                for (int i = (int)k.size() - 1; i >= 0; --i)
+                    if (is_inner(k[i])) st.push_back(wide_of[k[i]]);
+            }
+        }
+        if (!is_inner(0)) place(0);
+        for (int32_t t = 0; t < hs.ntri; ++t)
+            if (pos[t] < 0) pos[t] = next++;   // unreachable triangles and RT_TRI_ORDER 0 keep their order
+        hs.tri_fast.assign(hs.tri_geo.size(), 0.0f);
+        for (int32_t t = 0; t < hs.ntri; ++t)
+            for (int k = 0; k < 12; ++k) hs.tri_fast[12 * (size_t)pos[t] + k] = hs.tri_geo[12 * (size_t)t + k];
+    }
     hs.nnodes = (int32_t)bfs.size();
     hs.nodes.assign((size_t)hs.nnodes * F, 0.0f);
     for (size_t w = 0; w < bfs.size(); ++w) {
         float* o = hs.nodes.data() + (size_t)F * w;
         const auto& ch = children[w];
-        auto ref = [&](int32_t c) { return is_inner(c) ? wide_of[c] : ~(48 * T[c]); };
+        auto ref = [&](int32_t c) { return is_inner(c) ? wide_of[c] : ~(48 * pos[T[c]]); };
         if (W == 2) {
             const float* c0 = box + 6 * (int64_t)ch[0];
             const float* c1 = box + 6 * (int64_t)ch[1];
@@ -274,7 +304,7 @@ void emit_bvh(HostScene& hs, const int32_t* L, const int32_t* R, const int32_t* 
             }
         }
     }
-    hs.root_ref = is_inner(0) ? 0 : ~(48 * T[0]);
+    hs.root_ref = is_inner(0) ? 0 : ~(48 * pos[T[0]]);
     // compact item layout of the item-step tree walk (rt_internal.h DevScene::nodes48 / tri2): a node
     // is its 48 bytes of child boxes; the ref of an internal child ((BFS index << 2) | its child-is-leaf
     // bits) is written into the low 4 bits of that child's six box coordinates, each moved outwards
@@ -391,7 +421,10 @@ bool pack_fast(HostScene& hs, const float* bvh9, int64_t nn, int64_t ntri, int l
             if (R[n] >= 0) st.push_back(R[n]);
         }
     }
-    for (int64_t t = 0; t < ntri; ++t) hs.tri_geo[12 * t + 3] = as_f32(rank[t]);
+    for (int64_t t = 0; t < ntri; ++t) {
+        hs.tri_geo[12 * t + 3] = as_f32(rank[t]);
+        hs.tri_geo[12 * t + 7] = as_f32((int32_t)t);   // e1.w: the triangle's own index (FAST hit records)
+    }
     // small scenes: brute-force records of the reachable triangles in DFS-rank order
     hs.brute.clear();
     hs.brute_box.clear();
@@ -519,6 +552,7 @@ rt::DevScene dev_scene(const rt_ctx* ctx, const Device& d) {
     s.bvh9 = (const float*)d.bvh9.p;
     s.nbvh9 = ctx->hs.nbvh9;
     s.tri_geo = (const float4*)d.tri_geo.p;
+    s.tri_fast = (const float4*)d.tri_fast.p;
     s.tri_shade = (const float4*)d.tri_shade.p;
     s.tri_frame = (const float4*)d.tri_frame.p;
     s.ntri = ctx->hs.ntri;
@@ -619,7 +653,7 @@ void rt_destroy(rt_ctx* ctx) {
     for (auto& d : ctx->devs) {
         if (hipSetDevice(d.id) != hipSuccess) continue;
         if (d.stream) (void)hipStreamSynchronize(d.stream);
-        for (DevBuf* b : {&d.stack_ovf, &d.nodes, &d.nodes48, &d.tri2, &d.brute, &d.brute_box, &d.bvh9, &d.tri_geo, &d.tri_shade, &d.tri_frame, &d.mat, &d.ibl, &d.out,
+        for (DevBuf* b : {&d.stack_ovf, &d.nodes, &d.nodes48, &d.tri2, &d.tri_fast, &d.brute, &d.brute_box, &d.bvh9, &d.tri_geo, &d.tri_shade, &d.tri_frame, &d.mat, &d.ibl, &d.out,
                           &d.counts, &d.work, &d.scratch_a, &d.scratch_b})
             release(*b);
         if (d.host_stage) (void)hipHostFree(d.host_stage);
@@ -659,6 +693,7 @@ int rt_set_option(rt_ctx* ctx, const char* key, int64_t value) {
             HIP_OR_RET(ctx, upload(d.brute, hs.brute, d.stream));
             HIP_OR_RET(ctx, upload(d.brute_box, hs.brute_box, d.stream));
             HIP_OR_RET(ctx, upload(d.tri_geo, hs.tri_geo, d.stream));
+            HIP_OR_RET(ctx, upload(d.tri_fast, hs.tri_fast, d.stream));
             HIP_OR_RET(ctx, ensure_stack_ovf(d, hs));
             HIP_OR_RET(ctx, hipStreamSynchronize(d.stream));
         }
@@ -804,6 +839,7 @@ int rt_set_scene(rt_ctx* ctx, const float* vp, int64_t nvp, const float* vn, int
         HIP_OR_RET(ctx, ensure_stack_ovf(d, hs));
         HIP_OR_RET(ctx, upload(d.bvh9, hs.bvh9, d.stream));
         HIP_OR_RET(ctx, upload(d.tri_geo, hs.tri_geo, d.stream));
+        HIP_OR_RET(ctx, upload(d.tri_fast, hs.tri_fast, d.stream));
         HIP_OR_RET(ctx, upload(d.tri_shade, hs.tri_shade, d.stream));
         HIP_OR_RET(ctx, upload(d.mat, hs.mat, d.stream));
         HIP_OR_RET(ctx, ensure(d.tri_frame, (size_t)std::max<int64_t>(T, 1) * 3 * sizeof(float4)));

@@ -56,8 +56,11 @@ struct DevScene {
     // REF traversal: the reference's own AoS export, 9 floats per node
     const float* bvh9;
     int32_t nbvh9;
-    // triangles in reference order: 3 x float4 (a.p | rank, e1 | 0, e2 | 0)
+    // triangles in reference order: 3 x float4 (a.p | rank, e1 | index, e2 | 0); REF traversal
     const float4* tri_geo;
+    // the same records in the order the FAST tree's leaves are met depth-first (the FAST leaf refs
+    // are byte offsets into this array; e1.w gives the triangle's reference index)
+    const float4* tri_fast;
     // hit record per triangle: first-vertex normal | material index bits
     const float4* tri_shade;
     // hemisphere frame per triangle (prep_frames_kernel): q, qinv, normalize(n) | colinear flag

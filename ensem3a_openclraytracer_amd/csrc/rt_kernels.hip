@@ -174,10 +174,11 @@ __device__ __forceinline__ bool mt_vals(float4 g0, float4 g1, float4 g2, rtm_f3 
 // and no nested divergence per triangle.
 // tb + toff: the triangle's 48-byte record (toff = 48 * t, 32-bit: no 64-bit multiply in the loop).
 __device__ __forceinline__ bool mt_flat(const char* __restrict__ tb, unsigned toff, rtm_f3 o, rtm_f3 d, float* kout,
-                                        int* rank) {
+                                        int* rank, int* index) {
     const float4 g0 = *reinterpret_cast<const float4*>(tb + toff);
     const float4 g1 = *reinterpret_cast<const float4*>(tb + toff + 16);
     const float4 g2 = *reinterpret_cast<const float4*>(tb + toff + 32);
+    *index = __float_as_int(g1.w);   // the triangle's reference index (DevScene::tri_fast)
     return mt_vals(g0, g1, g2, o, d, kout, rank);
 }
 
@@ -366,10 +367,11 @@ __device__ Hit trace_fast(const DevScene& S, const float4* __restrict__ nodes, c
             float k;
             int rank;
             const unsigned toff = ~(unsigned)item;   // leaf ref = ~(48 * triangle)
-            if (mt_flat(tb, toff, o, d, &k, &rank) && k > 0.0001f &&
+            int index;
+            if (mt_flat(tb, toff, o, d, &k, &rank, &index) && k > 0.0001f &&
                 (k < best.k || (k == best.k && rank < best_rank))) {
                 best.k = k;
-                best.tri = (int)toff;
+                best.tri = 48 * index;
                 best_rank = rank;
             }
         }
@@ -966,13 +968,13 @@ __global__ void RT_RENDER_BOUNDS render_kernel(DevScene S, FrameParams F, float*
     // SMEM: the whole BVH2 node array and triangle array of a small scene are
     // staged in LDS behind the stacks, once per (persistent) block.
     const float4* nodes = S.nodes;
-    const float4* tris = S.tri_geo;
+    const float4* tris = S.tri_fast;
     if (SMEM) {
         float4* ln = reinterpret_cast<float4*>(lds_stack + 2 * S.stack_lds * B);
         float4* lt = ln + kNodeF4 * S.nnodes;
         for (int q = threadIdx.x; q < kNodeF4 * S.nnodes; q += B)
             ln[(q % kNodeF4) * S.nnodes + q / kNodeF4] = S.nodes[q];
-        for (int q = threadIdx.x; q < 3 * S.ntri; q += B) lt[q] = S.tri_geo[q];
+        for (int q = threadIdx.x; q < 3 * S.ntri; q += B) lt[q] = S.tri_fast[q];
         __syncthreads();
         nodes = ln;
         tris = lt;
@@ -1237,10 +1239,11 @@ __device__ __forceinline__ bool fast_round(const DevScene& S, FastRay& R, const 
         float k;
         int rank;
         const unsigned toff = ~(unsigned)R.item;
-        if (mt_flat(tb, toff, R.o, R.d, &k, &rank) && k > 0.0001f &&
+        int index;
+        if (mt_flat(tb, toff, R.o, R.d, &k, &rank, &index) && k > 0.0001f &&
             (k < R.bk || (k == R.bk && rank < R.brank))) {
             R.bk = k;
-            R.bt = (int)toff;
+            R.bt = 48 * index;
             R.brank = rank;
             if (R.any) return true;
         }
@@ -1303,7 +1306,7 @@ __device__ __forceinline__ bool fast_step(const DevScene& S, FastRay& R, const c
         int rank;
         if (mt_vals(g0, g1, g2, R.o, R.d, &k, &rank) && k > 0.0001f && (k < R.bk || (k == R.bk && rank < R.brank))) {
             R.bk = k;
-            R.bt = COMPACT ? 48 * __float_as_int(g1.w) : (int)~(unsigned)R.item;
+            R.bt = 48 * __float_as_int(g1.w);   // e1.w: the triangle's reference index
             R.brank = rank;
             if (R.any) return true;
         }
@@ -1349,13 +1352,13 @@ __global__ void RT_RESUME_BOUNDS render_resume_kernel(DevScene S, FrameParams F,
     Cnt c{0, 0, 0, 0, 0, 0, 0, 0, 0};
     const LaunchConst& C = *lconst;
     const float4* nodes = S.nodes;
-    const float4* tris = S.tri_geo;
+    const float4* tris = S.tri_fast;
     if (SMEM) {
         float4* ln = reinterpret_cast<float4*>(lds_stack + 2 * S.stack_lds * B);
         float4* lt = ln + kNodeF4 * S.nnodes;
         for (int q = threadIdx.x; q < kNodeF4 * S.nnodes; q += B)
             ln[(q % kNodeF4) * S.nnodes + q / kNodeF4] = S.nodes[q];
-        for (int q = threadIdx.x; q < 3 * S.ntri; q += B) lt[q] = S.tri_geo[q];
+        for (int q = threadIdx.x; q < 3 * S.ntri; q += B) lt[q] = S.tri_fast[q];
         __syncthreads();
         nodes = ln;
         tris = lt;
@@ -1708,7 +1711,7 @@ __global__ void __launch_bounds__(256) debug_trace_kernel(DevScene S, const floa
     if (t >= n) return;
     Cnt c{0, 0, 0, 0, 0, 0, 0, 0, 0};
     const float* r = rays + 6 * t;
-    const Hit h = trace<TRAV, false>(S, S.nodes, S.tri_geo, rtm_v3(r[3], r[4], r[5]), rtm_v3(r[0], r[1], r[2]),
+    const Hit h = trace<TRAV, false>(S, S.nodes, S.tri_fast, rtm_v3(r[3], r[4], r[5]), rtm_v3(r[0], r[1], r[2]),
                                      lds_stack + threadIdx.x, blockDim.x, lane_stack(S, lds_stack), c);
     out[2 * t + 0] = h.k;
     out[2 * t + 1] = (float)h.tri;
