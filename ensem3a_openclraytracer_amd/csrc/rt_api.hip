@@ -28,15 +28,6 @@
 #ifndef RT_RESUME_MIN_DEFAULT
 #define RT_RESUME_MIN_DEFAULT 40  // FAST tree walk: resumable traversal threshold (rt_set_option "resume_min")
 #endif
-#ifndef RT_TRI_ORDER
-#define RT_TRI_ORDER 1         // FAST triangle records: 1 in the tree's depth-first leaf order, 0 reference order
-#endif
-#ifndef RT_COMPACT_DEFAULT
-#define RT_COMPACT_DEFAULT 0   // option "compact"
-#endif
-#ifndef RT_NODE_ORDER
-#define RT_NODE_ORDER 0        // FAST node numbering: 0 breadth-first, 1 depth-first preorder
-#endif
 #ifndef RT_BRUTE_MAX_DEFAULT
 #define RT_BRUTE_MAX_DEFAULT 64   // FAST tests every triangle of scenes up to this size (rt_set_option "brute_max")
 #endif
@@ -55,17 +46,21 @@ struct Device {
     hipStream_t stream = nullptr;
     int cus = 0;                  // compute units (sizes the FAST stack overflow buffer)
     DevBuf stack_ovf;             // FAST traversal stack entries beyond the LDS part
-    DevBuf nodes, nodes48, tri2, tri_fast, brute, brute_box, bvh9, tri_geo, tri_shade, tri_frame, mat, ibl, out, out8, counts, work, scratch_a, scratch_b;
+    DevBuf nodes, tri_fast, brute, brute_box, bvh9, tri_geo, tri_shade, tri_frame, mat, ibl, out, out8, counts, work, scratch_a, scratch_b;
     char* host_stage = nullptr;   // pinned staging for rt_render / rt_render_rgb8
     size_t host_stage_bytes = 0;
+    // Every launch of this context on the device shares `work` (pixel counters + launch constants)
+    // and reads the scene buffers, so launches are ordered across streams: `done` is recorded after
+    // each launch on its stream `last`; a launch on another stream, and every scene / IBL upload,
+    // first waits for it (order_after_last).
+    hipEvent_t done = nullptr;
+    hipStream_t last = nullptr;
+    bool pending = false;
 };
 
 // Host copy of the packed scene (kept to upload on every device).
 struct HostScene {
     std::vector<float> nodes;      // 16 floats per internal node
-    std::vector<float> nodes48;    // 12 floats per internal node, child refs in the box bits (DevScene::nodes48)
-    std::vector<float> tri2;       // 24 floats per internal node: its leaf children's records (DevScene::tri2)
-    int32_t root_ref48 = 0;
     std::vector<float> bvh9;
     std::vector<float> tri_geo;    // 12 floats per triangle
     std::vector<float> tri_fast;   // tri_geo's records in FAST leaf order (DevScene::tri_fast)
@@ -99,7 +94,6 @@ struct rt_ctx {
     int step = 0;       // tree-walk traversal loop: 0 auto, 1 one item per step, 2 descend-until-leaf rounds
     int sun_skip = 1;   // FAST: do not trace shadow rays of an unlit sun (FrameParams::sun_skip)
     int sun_any = 1;    // FAST tree walk: shadow rays end at their first hit when no material is glass
-    int compact = RT_COMPACT_DEFAULT;   // item-step tree walk on the compact node layout (DevScene::nodes48)
     int block = 128;
     std::string err;
 };
@@ -165,115 +159,56 @@ inline bool fidx(float v, int64_t limit, int32_t* out) {
     return true;
 }
 
-// Move v outwards (down for a lower bound, up for an upper bound) to the nearest float whose low 4
-// bits are nib.  False if no finite such float is close.
-bool embed_nibble(float& v, uint32_t nib, bool lower) {
-    float f = v;
-    for (int i = 0; i < 64; ++i) {
-        if (!std::isfinite(f)) return false;
-        uint32_t b;
-        std::memcpy(&b, &f, 4);
-        if ((b & 15u) == nib) {
-            v = f;
-            return true;
-        }
-        f = std::nextafter(f, lower ? -INFINITY : INFINITY);
-    }
-    return false;
-}
-
-// Emit the FAST node array from a binary tree with one triangle per leaf:
-// internal nodes in BFS order, each holding its children's boxes and refs.
+// Emit the FAST node array from a binary tree with one triangle per leaf: internal nodes in BFS
+// order, each holding its two children's boxes and refs (rt_internal.h DevScene::nodes).
 // box: 6 floats per tree node (lo.xyz, hi.xyz).
-//   RT_BVH_WIDTH 2: a node = its two children (rt_internal.h DevScene::nodes).
-//   RT_BVH_WIDTH 4: the binary tree is collapsed (an internal child with the largest
-//   surface area is replaced by its two children while fewer than 4), a node =
-//   8 float4: lo.x[4] hi.x[4] lo.y[4] hi.y[4] lo.z[4] hi.z[4] refs[4] unused; empty
-//   slots get a +inf box, which no slab test accepts.  Leaf boxes stay the reference's.
 void emit_bvh(HostScene& hs, const int32_t* L, const int32_t* R, const int32_t* T, const float* box, int64_t nn) {
-    constexpr int W = RT_BVH_WIDTH;
+    (void)nn;
     auto is_inner = [&](int64_t i) { return L[i] >= 0; };
-    auto area = [&](int64_t i) {
-        const float* b = box + 6 * i;
-        const double x = (double)b[3] - b[0], y = (double)b[4] - b[1], z = (double)b[5] - b[2];
-        return x * y + y * z + z * x;
-    };
-    auto kids = [&](int32_t n) {
-        std::vector<int32_t> k{L[n], R[n]};
-        while ((int)k.size() < W) {
-            int best = -1;
-            for (int i = 0; i < (int)k.size(); ++i)
-                if (is_inner(k[i]) && (best < 0 || area(k[i]) > area(k[best]))) best = i;
-            if (best < 0) break;
-            const int32_t c = k[best];
-            k[best] = L[c];
-            k.insert(k.begin() + best + 1, R[c]);
-        }
-        return k;
-    };
     std::vector<int32_t> wide_of(nn, -1), bfs;
-    std::vector<std::vector<int32_t>> children;
-#if RT_NODE_ORDER == 1
-    // depth-first preorder: every subtree's nodes are contiguous
-    if (is_inner(0)) {
-        std::vector<int32_t> st{0};
-        while (!st.empty()) {
-            const int32_t n = st.back();
-            st.pop_back();
-            wide_of[n] = (int32_t)bfs.size();
-            bfs.push_back(n);
-            children.push_back(kids(n));
-            const std::vector<int32_t>& k = children.back();
-            for (int i = (int)k.size() - 1; i >= 0; --i)
-                if (is_inner(k[i])) st.push_back(k[i]);
-        }
-    }
-#else
     if (is_inner(0)) {
         bfs.push_back(0);
         wide_of[0] = 0;
     }
     for (size_t h = 0; h < bfs.size(); ++h) {
-        children.push_back(kids(bfs[h]));
-        for (int32_t ch : children.back()) {
+        for (int32_t ch : {L[bfs[h]], R[bfs[h]]}) {
             if (!is_inner(ch)) continue;
             wide_of[ch] = (int32_t)bfs.size();
             bfs.push_back(ch);
         }
     }
-#endif
-    // stack bound: a node pushes (children - 1) entries at most; need = max over root-to-leaf
-    // paths of the sum (children are after their parents in BFS order: sweep backwards)
+    // stack bound: a node pushes one entry at most; need = max over root-to-leaf paths of the sum
+    // (children are after their parents in BFS order: sweep backwards)
     std::vector<int32_t> need(bfs.size(), 0);
     for (size_t w = bfs.size(); w-- > 0;) {
         int32_t sub = 0;
-        for (int32_t ch : children[w])
+        for (int32_t ch : {L[bfs[w]], R[bfs[w]]})
             if (is_inner(ch)) sub = std::max(sub, need[wide_of[ch]]);
-        need[w] = (int32_t)children[w].size() - 1 + sub;
+        need[w] = 1 + sub;
     }
-    constexpr int F = 4 * (W == 4 ? 8 : 4);   // floats per node
+    constexpr int F = 4 * rt::kNodeF4;   // floats per node
     // the FAST traversal's triangle records (DevScene::tri_fast), in the order a depth-first walk of
-    // this tree meets its leaves (RT_TRI_ORDER 1) or in reference order (0): pos[t] = record of t
+    // this tree meets its leaves: pos[t] = record of t
     std::vector<int32_t> pos((size_t)hs.ntri, -1);
     {
         int32_t next = 0;
         auto place = [&](int32_t c) {
             if (!is_inner(c) && T[c] >= 0 && pos[T[c]] < 0) pos[T[c]] = next++;
         };
-        if (RT_TRI_ORDER == 1 && is_inner(0)) {
+        if (is_inner(0)) {
             std::vector<int32_t> st{0};
             while (!st.empty()) {
-                const int32_t w = st.back();
+                const int32_t n = st.back();
                 st.pop_back();
-                const auto& k = children[w];
-                for (int32_t c : k) place(c);
-                for (int i = (int)k.size() - 1; i >= 0; --i)
-                    if (is_inner(k[i])) st.push_back(wide_of[k[i]]);
+                place(L[n]);
+                place(R[n]);
+                if (is_inner(R[n])) st.push_back(R[n]);
+                if (is_inner(L[n])) st.push_back(L[n]);
             }
         }
         if (!is_inner(0)) place(0);
         for (int32_t t = 0; t < hs.ntri; ++t)
-            if (pos[t] < 0) pos[t] = next++;   // unreachable triangles and RT_TRI_ORDER 0 keep their order
+            if (pos[t] < 0) pos[t] = next++;   // unreachable triangles keep their order
         hs.tri_fast.assign(hs.tri_geo.size(), 0.0f);
         for (int32_t t = 0; t < hs.ntri; ++t)
             for (int k = 0; k < 12; ++k) hs.tri_fast[12 * (size_t)pos[t] + k] = hs.tri_geo[12 * (size_t)t + k];
@@ -282,69 +217,16 @@ void emit_bvh(HostScene& hs, const int32_t* L, const int32_t* R, const int32_t* 
     hs.nodes.assign((size_t)hs.nnodes * F, 0.0f);
     for (size_t w = 0; w < bfs.size(); ++w) {
         float* o = hs.nodes.data() + (size_t)F * w;
-        const auto& ch = children[w];
+        const int32_t n = bfs[w];
         auto ref = [&](int32_t c) { return is_inner(c) ? wide_of[c] : ~(48 * pos[T[c]]); };
-        if (W == 2) {
-            const float* c0 = box + 6 * (int64_t)ch[0];
-            const float* c1 = box + 6 * (int64_t)ch[1];
-            o[0] = c0[0]; o[1] = c0[3]; o[2] = c0[1]; o[3] = c0[4];
-            o[4] = c1[0]; o[5] = c1[3]; o[6] = c1[1]; o[7] = c1[4];
-            o[8] = c0[2]; o[9] = c0[5]; o[10] = c1[2]; o[11] = c1[5];
-            o[12] = as_f32(ref(ch[0])); o[13] = as_f32(ref(ch[1])); o[14] = 0.0f; o[15] = 0.0f;
-        } else {
-            for (int i = 0; i < 4; ++i) {
-                const bool used = i < (int)ch.size();
-                const float* b = used ? box + 6 * (int64_t)ch[i] : nullptr;
-                for (int a = 0; a < 3; ++a) {
-                    o[8 * a + i] = used ? b[a] : INFINITY;          // lo
-                    o[8 * a + 4 + i] = used ? b[3 + a] : INFINITY;  // hi
-                }
-                o[24 + i] = as_f32(used ? ref(ch[i]) : INT32_MIN);
-                o[28 + i] = 0.0f;
-            }
-        }
+        const float* c0 = box + 6 * (int64_t)L[n];
+        const float* c1 = box + 6 * (int64_t)R[n];
+        o[0] = c0[0]; o[1] = c0[3]; o[2] = c0[1]; o[3] = c0[4];
+        o[4] = c1[0]; o[5] = c1[3]; o[6] = c1[1]; o[7] = c1[4];
+        o[8] = c0[2]; o[9] = c0[5]; o[10] = c1[2]; o[11] = c1[5];
+        o[12] = as_f32(ref(L[n])); o[13] = as_f32(ref(R[n])); o[14] = 0.0f; o[15] = 0.0f;
     }
     hs.root_ref = is_inner(0) ? 0 : ~(48 * pos[T[0]]);
-    // compact item layout of the item-step tree walk (rt_internal.h DevScene::nodes48 / tri2): a node
-    // is its 48 bytes of child boxes; the ref of an internal child ((BFS index << 2) | its child-is-leaf
-    // bits) is written into the low 4 bits of that child's six box coordinates, each moved outwards
-    // to the nearest float with the wanted bits (an internal box only prunes, a larger one prunes
-    // less: same hits); leaf boxes stay exact and a leaf child's triangle record sits at slot 2 w + c
-    hs.nodes48.clear();
-    hs.tri2.clear();
-    hs.root_ref48 = 0;
-    if (W == 2 && is_inner(0) && bfs.size() < (size_t)1 << 22) {
-        auto types = [&](size_t w) {
-            return (uint32_t)(is_inner(children[w][0]) ? 0 : 1) | (uint32_t)(is_inner(children[w][1]) ? 0 : 2);
-        };
-        bool ok = true;
-        constexpr size_t CS = rt::kCompactStride / 4;   // floats per record
-        hs.nodes48.assign(bfs.size() * CS, 0.0f);
-        hs.tri2.assign(bfs.size() * 2 * CS, 0.0f);
-        for (size_t w = 0; w < bfs.size() && ok; ++w) {
-            float* q = hs.nodes48.data() + CS * w;
-            for (int k = 0; k < 12; ++k) q[k] = hs.nodes[(size_t)F * w + k];
-            for (int c = 0; c < 2 && ok; ++c) {
-                const int32_t ch = children[w][c];
-                if (is_inner(ch)) {
-                    const uint32_t r = ((uint32_t)wide_of[ch] << 2) | types((size_t)wide_of[ch]);
-                    // the child's lo.x hi.x lo.y hi.y lo.z hi.z in the node
-                    const int at[6] = {4 * c, 4 * c + 1, 4 * c + 2, 4 * c + 3, 8 + 2 * c, 9 + 2 * c};
-                    for (int k = 0; k < 6 && ok; ++k) ok = embed_nibble(q[at[k]], (r >> (4 * k)) & 15u, (k & 1) == 0);
-                } else {
-                    float* t2 = hs.tri2.data() + CS * (2 * w + c);
-                    for (int k = 0; k < 12; ++k) t2[k] = hs.tri_geo[12 * (size_t)T[ch] + k];
-                    t2[7] = as_f32(T[ch]);   // e1.w: the triangle index
-                }
-            }
-        }
-        if (ok) {
-            hs.root_ref48 = (int32_t)types(0);
-        } else {
-            hs.nodes48.clear();
-            hs.tri2.clear();
-        }
-    }
     for (int k = 0; k < 6; ++k) hs.root_box[k] = box[k];
     hs.depth = bfs.empty() ? 1 : std::max(1, need[0]);
 }
@@ -458,7 +340,7 @@ bool pack_fast(HostScene& hs, const float* bvh9, int64_t nn, int64_t ntri, int l
                 std::array<uint32_t, 6> key;
                 for (int k = 0; k < 6; ++k) std::memcpy(&key[k], r + k, 4);
                 auto it = open.find(key);
-                if (RT_BOX_DEDUP && it != open.end()) {
+                if (it != open.end()) {
                     groups[it->second][1] = (int32_t)q;
                     open.erase(it);
                 } else {
@@ -532,6 +414,17 @@ hipError_t ensure_stack_ovf(Device& d, const HostScene& hs) {
     return ensure(d.stack_ovf, (size_t)std::max(d.cus, 1) * rt::kMaxLanesPerCu * (size_t)extra * sizeof(int2));
 }
 
+hipError_t order_after_last(Device& d, hipStream_t s) {
+    if (d.pending && d.last != s) return hipStreamWaitEvent(s, d.done, 0);
+    return hipSuccess;
+}
+
+hipError_t mark_launch(Device& d, hipStream_t s) {
+    d.last = s;
+    d.pending = true;
+    return hipEventRecord(d.done, s);
+}
+
 template <typename T>
 hipError_t upload(DevBuf& b, const std::vector<T>& v, hipStream_t s) {
     const size_t bytes = v.size() * sizeof(T);
@@ -543,9 +436,6 @@ hipError_t upload(DevBuf& b, const std::vector<T>& v, hipStream_t s) {
 rt::DevScene dev_scene(const rt_ctx* ctx, const Device& d) {
     rt::DevScene s{};
     s.nodes = (const float4*)d.nodes.p;
-    s.nodes48 = ctx->hs.nodes48.empty() ? nullptr : (const float4*)d.nodes48.p;
-    s.tri2 = ctx->hs.tri2.empty() ? nullptr : (const float4*)d.tri2.p;
-    s.root_ref48 = ctx->hs.root_ref48;
     s.nnodes = ctx->hs.nnodes;
     s.root_ref = ctx->hs.root_ref;
     for (int k = 0; k < 6; ++k) s.root_box[k] = ctx->hs.root_box[k];
@@ -595,7 +485,6 @@ int check_frame(rt_ctx* ctx, const float* cam, const float* env, int64_t npix, i
     fp->step = ctx->step;
     fp->sun_skip = (ctx->sun_skip && env[3] == 0.0f && env[4] >= 0.0f && ctx->hs.colors_finite) ? 1 : 0;
     fp->sun_any = (ctx->sun_any && !ctx->hs.has_glass) ? 1 : 0;
-    fp->compact = ctx->compact;
     fp->team = ctx->team;
     fp->max_waves = ctx->max_waves;
     fp->log_buf = nullptr;
@@ -639,6 +528,7 @@ int rt_create(int n_devices, const int* device_ids, rt_ctx** out) {
         ctx->devs[i].id = id;
         if ((e = hipSetDevice(id)) != hipSuccess ||
             (e = hipStreamCreateWithFlags(&ctx->devs[i].stream, hipStreamNonBlocking)) != hipSuccess ||
+            (e = hipEventCreateWithFlags(&ctx->devs[i].done, hipEventDisableTiming)) != hipSuccess ||
             (e = hipDeviceGetAttribute(&ctx->devs[i].cus, hipDeviceAttributeMultiprocessorCount, id)) != hipSuccess) {
             rt_destroy(ctx);
             return set_err(nullptr, RT_ERR_HIP, "device %d init failed: %s", id, hipGetErrorString(e));
@@ -652,12 +542,14 @@ void rt_destroy(rt_ctx* ctx) {
     if (!ctx) return;
     for (auto& d : ctx->devs) {
         if (hipSetDevice(d.id) != hipSuccess) continue;
+        if (d.pending) (void)hipEventSynchronize(d.done);
         if (d.stream) (void)hipStreamSynchronize(d.stream);
-        for (DevBuf* b : {&d.stack_ovf, &d.nodes, &d.nodes48, &d.tri2, &d.tri_fast, &d.brute, &d.brute_box, &d.bvh9, &d.tri_geo, &d.tri_shade, &d.tri_frame, &d.mat, &d.ibl, &d.out,
+        for (DevBuf* b : {&d.stack_ovf, &d.nodes, &d.tri_fast, &d.brute, &d.brute_box, &d.bvh9, &d.tri_geo, &d.tri_shade, &d.tri_frame, &d.mat, &d.ibl, &d.out,
                           &d.counts, &d.work, &d.scratch_a, &d.scratch_b})
             release(*b);
         if (d.host_stage) (void)hipHostFree(d.host_stage);
         if (d.stream) (void)hipStreamDestroy(d.stream);
+        if (d.done) (void)hipEventDestroy(d.done);
     }
     delete ctx;
 }
@@ -687,9 +579,8 @@ int rt_set_option(rt_ctx* ctx, const char* key, int64_t value) {
         pack_checked(hs, hs.bvh9.data(), hs.nbvh9, hs.ntri, ctx->bvh_layout, ctx->brute_max, why);
         for (auto& d : ctx->devs) {
             HIP_OR_RET(ctx, hipSetDevice(d.id));
+            HIP_OR_RET(ctx, order_after_last(d, d.stream));
             HIP_OR_RET(ctx, upload(d.nodes, hs.nodes, d.stream));
-            HIP_OR_RET(ctx, upload(d.nodes48, hs.nodes48, d.stream));
-            HIP_OR_RET(ctx, upload(d.tri2, hs.tri2, d.stream));
             HIP_OR_RET(ctx, upload(d.brute, hs.brute, d.stream));
             HIP_OR_RET(ctx, upload(d.brute_box, hs.brute_box, d.stream));
             HIP_OR_RET(ctx, upload(d.tri_geo, hs.tri_geo, d.stream));
@@ -709,11 +600,6 @@ int rt_set_option(rt_ctx* ctx, const char* key, int64_t value) {
         if (value != 0 && value != 1 && value != 2 && value != 4 && value != 8)
             return set_err(ctx, RT_ERR_ARG, "team must be 0 (auto), 1, 2, 4 or 8");
         ctx->team = (int)value;
-        return RT_OK;
-    }
-    if (!std::strcmp(key, "compact")) {
-        if (value != 0 && value != 1) return set_err(ctx, RT_ERR_ARG, "compact must be 0 or 1");
-        ctx->compact = (int)value;
         return RT_OK;
     }
     if (!std::strcmp(key, "sun_any")) {
@@ -831,9 +717,8 @@ int rt_set_scene(rt_ctx* ctx, const float* vp, int64_t nvp, const float* vn, int
     pack_checked(hs, bvh9, NB, T, ctx->bvh_layout, ctx->brute_max, why);
     for (auto& d : ctx->devs) {
         HIP_OR_RET(ctx, hipSetDevice(d.id));
+        HIP_OR_RET(ctx, order_after_last(d, d.stream));
         HIP_OR_RET(ctx, upload(d.nodes, hs.nodes, d.stream));
-        HIP_OR_RET(ctx, upload(d.nodes48, hs.nodes48, d.stream));
-        HIP_OR_RET(ctx, upload(d.tri2, hs.tri2, d.stream));
         HIP_OR_RET(ctx, upload(d.brute, hs.brute, d.stream));
         HIP_OR_RET(ctx, upload(d.brute_box, hs.brute_box, d.stream));
         HIP_OR_RET(ctx, ensure_stack_ovf(d, hs));
@@ -843,7 +728,7 @@ int rt_set_scene(rt_ctx* ctx, const float* vp, int64_t nvp, const float* vn, int
         HIP_OR_RET(ctx, upload(d.tri_shade, hs.tri_shade, d.stream));
         HIP_OR_RET(ctx, upload(d.mat, hs.mat, d.stream));
         HIP_OR_RET(ctx, ensure(d.tri_frame, (size_t)std::max<int64_t>(T, 1) * 3 * sizeof(float4)));
-        HIP_OR_RET(ctx, ensure(d.work, 1024));
+        HIP_OR_RET(ctx, ensure(d.work, rt::kWorkBytes));
         HIP_OR_RET(ctx, hipStreamSynchronize(d.stream));
     }
     ctx->hs = std::move(hs);
@@ -863,6 +748,8 @@ int rt_set_env(rt_ctx* ctx, const uint8_t* rgba, int w, int h) {
     const size_t bytes = (size_t)w * h * 4;
     for (auto& d : ctx->devs) {
         HIP_OR_RET(ctx, hipSetDevice(d.id));
+        HIP_OR_RET(ctx, order_after_last(d, d.stream));
+        HIP_OR_RET(ctx, hipStreamSynchronize(d.stream));   // the old IBL buffer may be freed by ensure
         HIP_OR_RET(ctx, ensure(d.ibl, bytes));
         HIP_OR_RET(ctx, hipMemcpyAsync(d.ibl.p, rgba, bytes, hipMemcpyHostToDevice, d.stream));
         HIP_OR_RET(ctx, hipStreamSynchronize(d.stream));
@@ -893,8 +780,10 @@ int rt_render_device(rt_ctx* ctx, int device_index, const float cam[10], const f
     Device& d = ctx->devs[device_index];
     HIP_OR_RET(ctx, hipSetDevice(d.id));
     hipStream_t s = (hipStream_t)stream;  // NULL = the device's default (null) stream, HIP convention
+    HIP_OR_RET(ctx, order_after_last(d, s));
     HIP_OR_RET(ctx, rt::launch_render(dev_scene(ctx, d), fp, effective_traversal(ctx), ctx->block, d_out, nullptr,
                                       (unsigned int*)d.work.p, s));
+    HIP_OR_RET(ctx, mark_launch(d, s));
     return RT_OK;
 }
 
@@ -931,8 +820,10 @@ int render_host(rt_ctx* ctx, const float cam[10], const float env[5], int64_t np
             HIP_OR_RET(ctx, hipHostMalloc((void**)&d.host_stage, bytes, hipHostMallocDefault));
             d.host_stage_bytes = bytes;
         }
+        HIP_OR_RET(ctx, order_after_last(d, d.stream));
         HIP_OR_RET(ctx, rt::launch_render(dev_scene(ctx, d), fp, effective_traversal(ctx), ctx->block,
                                           (float*)d.out.p, nullptr, (unsigned int*)d.work.p, d.stream));
+        HIP_OR_RET(ctx, mark_launch(d, d.stream));
         const void* src = d.out.p;
         if (rgb8 >= 0) {
             HIP_OR_RET(ctx, ensure(d.out8, bytes));
@@ -1020,8 +911,10 @@ int count_all(rt_ctx* ctx, const float cam[10], const float env[5], int64_t npix
     unsigned long long h[16] = {0};
     HIP_OR_RET(ctx, ensure(d.counts, sizeof h));
     HIP_OR_RET(ctx, hipMemsetAsync(d.counts.p, 0, sizeof h, d.stream));
+    HIP_OR_RET(ctx, order_after_last(d, d.stream));
     HIP_OR_RET(ctx, rt::launch_render(dev_scene(ctx, d), fp, effective_traversal(ctx), ctx->block, (float*)d.out.p,
                                       (unsigned long long*)d.counts.p, (unsigned int*)d.work.p, d.stream));
+    HIP_OR_RET(ctx, mark_launch(d, d.stream));
     HIP_OR_RET(ctx, hipMemcpyAsync(h, d.counts.p, sizeof h, hipMemcpyDeviceToHost, d.stream));
     HIP_OR_RET(ctx, hipStreamSynchronize(d.stream));
     for (int q = 0; q < n; ++q) counts[q] = h[q];
@@ -1043,7 +936,7 @@ int rt_work_bytes(rt_ctx* ctx, double out[4]) {
     // Algorithmic bytes per unit: 32 B per box test (24 B AABB + 8 B child/leaf
     // refs), 36 B per triangle test (v0, e1, e2), 40 B per hit record, 16 B per IBL lookup.
     if (!ctx || !out) return set_err(ctx, RT_ERR_ARG, "null argument");
-    out[0] = effective_traversal(ctx) == RT_TRAVERSAL_FAST ? 32.0 * RT_BVH_WIDTH  // a FAST node tests all its boxes
+    out[0] = effective_traversal(ctx) == RT_TRAVERSAL_FAST ? 64.0  // a FAST node tests both child boxes
                                                             : 32.0;                // one reference node = one box
     out[1] = 36.0;
     out[2] = 40.0;
@@ -1097,6 +990,7 @@ int rt_debug_trace(rt_ctx* ctx, int traversal, const float* rays, float* out, in
     HIP_OR_RET(ctx, ensure(d.scratch_a, (size_t)n * 6 * sizeof(float)));
     HIP_OR_RET(ctx, ensure(d.scratch_b, (size_t)n * 2 * sizeof(float)));
     HIP_OR_RET(ctx, hipMemcpyAsync(d.scratch_a.p, rays, (size_t)n * 6 * sizeof(float), hipMemcpyHostToDevice, d.stream));
+    HIP_OR_RET(ctx, order_after_last(d, d.stream));
     HIP_OR_RET(ctx, rt::launch_debug_trace(dev_scene(ctx, d), traversal, (const float*)d.scratch_a.p,
                                            (float*)d.scratch_b.p, n, d.stream));
     HIP_OR_RET(ctx, hipMemcpyAsync(out, d.scratch_b.p, (size_t)n * 2 * sizeof(float), hipMemcpyDeviceToHost, d.stream));
@@ -1128,7 +1022,9 @@ int rt_debug_pixel_log(rt_ctx* ctx, int traversal, const float cam[10], const fl
     fp.log_cap = cap;
     fp.log_pixel = pixel;
     HIP_OR_RET(ctx, hipMemsetAsync(fp.log_count, 0, sizeof(int32_t), d.stream));
+    HIP_OR_RET(ctx, order_after_last(d, d.stream));
     HIP_OR_RET(ctx, rt::launch_debug_log(dev_scene(ctx, d), fp, traversal, dout, (unsigned int*)d.work.p, d.stream));
+    HIP_OR_RET(ctx, mark_launch(d, d.stream));
     int32_t n = 0;
     HIP_OR_RET(ctx, hipMemcpyAsync(&n, fp.log_count, sizeof n, hipMemcpyDeviceToHost, d.stream));
     HIP_OR_RET(ctx, hipStreamSynchronize(d.stream));

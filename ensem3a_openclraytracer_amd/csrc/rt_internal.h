@@ -7,32 +7,22 @@
 namespace rt {
 
 // LDS entries of the FAST traversal stack per lane (int2 each); deeper entries spill to HBM.
-#ifndef RT_STACK_LDS
-#define RT_STACK_LDS 20
-#endif
-constexpr int kStackLds = RT_STACK_LDS;
-// FAST tree layout: 2 (BVH2, 4 float4 per node) or 4 (collapsed BVH4, 8 float4 per node)
-#ifndef RT_BVH_WIDTH
-#define RT_BVH_WIDTH 2
-#endif
-constexpr int kNodeF4 = RT_BVH_WIDTH == 4 ? 8 : 4;
+constexpr int kStackLds = 20;
+constexpr int kNodeF4 = 4;             // float4 per FAST BVH2 node (DevScene::nodes)
 constexpr int kMaxLanesPerCu = 2048;   // resident threads per CU (gfx950)
-// leaf boxes per scalar load group of the brute-force loop (DevScene::brute_box)
-#ifndef RT_BOX_GROUP
-#define RT_BOX_GROUP 4
-#endif
-constexpr int kBoxGroup = RT_BOX_GROUP;
-constexpr int kMatF = 8;   // floats per device material row (DevScene::mat)
-// bytes per node / per triangle record of the compact item layout (DevScene::nodes48, tri2): 48 B of
-// data each, 64 keeps them aligned to cache sectors
-#ifndef RT_COMPACT_STRIDE
-#define RT_COMPACT_STRIDE 64
-#endif
-constexpr int kCompactStride = RT_COMPACT_STRIDE;
-// brute-force records whose leaf boxes are bit-identical share one box test (DevScene::brute_box)
-#ifndef RT_BOX_DEDUP
-#define RT_BOX_DEDUP 1
-#endif
+constexpr int kBoxGroup = 4;           // leaf boxes per scalar load group of the brute-force loop (DevScene::brute_box)
+constexpr int kMatF = 8;               // floats per device material row (DevScene::mat)
+
+// Per-launch scratch block (the `work` argument of launch_render): pixel hand-out counters of the
+// kGroups block groups (blockIdx.x % kGroups: the blocks one XCD runs under round-robin dispatch),
+// kCounterStride bytes apart, then the per-launch constants at kConstOffset.
+constexpr int kGroups = 8;
+constexpr int kCounterStride = 64;
+constexpr int kConstOffset = 1024;
+constexpr int kWorkBytes = 2048;
+// Tile pixels are dealt to the groups in chunks of kChunk consecutive pixels (chunk c to group
+// c % kGroups), so each 128-byte line of the frame is written by the blocks of one XCD only.
+constexpr int kChunkShift = 10;
 
 // Device view of one uploaded scene (all pointers are device pointers).
 struct DevScene {
@@ -43,14 +33,6 @@ struct DevScene {
     //   [3] = child refs (int bits): >= 0 internal node, < 0 leaf = ~(48 * triangle), its tri_geo byte offset
     const float4* nodes;
     int32_t nnodes;        // internal nodes in `nodes`
-    // the same tree for the item-step walk, 3 x float4 per node (nullptr: not built): the first three
-    // float4 of `nodes`, where each internal child's six coordinates carry 4 bits of its ref in their
-    // low bits (moved outwards: a slightly larger box).  Refs: (BFS index << 2) | bit c set when child
-    // c is a leaf; a leaf child's ref is ~(48 * (2 * index + c)), the byte offset of its record in tri2
-    // (tri_geo's record with e1.w = the triangle index)
-    const float4* nodes48;
-    const float4* tri2;
-    int32_t root_ref48;
     int32_t root_ref;      // ref of the root (~(48 * tri) when the root is a leaf)
     float root_box[6];     // min.xyz, max.xyz of the root
     // REF traversal: the reference's own AoS export, 9 floats per node
@@ -108,7 +90,6 @@ struct FrameParams {
     // FAST tree walk: with no glass material the sun term depends only on whether the shadow ray hits
     // anything (Raytracing.cl:125-137), so its traversal ends at the first accepted triangle
     int32_t sun_any;
-    int32_t compact;     // item-step tree walk: use DevScene::nodes48 when built
     // debug event log of one pixel (rt_debug_pixel_log only; unused by the product launches)
     int64_t log_pixel;
     float* log_buf;
@@ -118,8 +99,7 @@ struct FrameParams {
 
 // Launch the render kernel; counts != nullptr selects the instrumented build
 // (device pointer to 5 uint64 accumulators).
-// d_work: >= 512 bytes of device scratch: the persistent kernel's pixel counter (zeroed by the
-// launch) followed by the per-launch constants block.
+// d_work: kWorkBytes of device scratch (layout above; the counters are zeroed by the launch).
 hipError_t launch_render(const DevScene& sc, const FrameParams& fp, int traversal, int block,
                          float* d_out, unsigned long long* d_counts, unsigned int* d_work, hipStream_t stream);
 hipError_t launch_prep_frames(const DevScene& sc, float4* frame, hipStream_t stream);

@@ -35,9 +35,7 @@ namespace rt {
 namespace {
 
 // Scenes whose BVH2 nodes + triangles take at most this many bytes are staged in LDS.
-#ifndef RT_LDS_SCENE_MAX
-#define RT_LDS_SCENE_MAX (24 * 1024)
-#endif
+constexpr size_t kLdsSceneMax = 24 * 1024;
 
 constexpr int TRAV_FAST = 0;
 constexpr int TRAV_REF = 1;
@@ -139,33 +137,24 @@ __device__ Hit trace_ref(const DevScene& S, rtm_f3 o, rtm_f3 d, int* __restrict_
 }
 
 // ---- FAST traversal ----
-// Slab test of one box against a ray given as inv = 1/d (and oi = o*inv).
-// RT_SLAB_FMA=1 uses one fma per plane, t = b*inv - o*inv, which cancels badly
-// when a direction component is tiny (|o/d| large); the default keeps the
-// reference's (b - o) scaled by 1/d.
-#ifndef RT_SLAB_FMA
-#define RT_SLAB_FMA 0
-#endif
-__device__ __forceinline__ void slab_fma(float lo_x, float hi_x, float lo_y, float hi_y, float lo_z, float hi_z,
-                                         float ox, float oy, float oz, float ix, float iy, float iz, float oix,
-                                         float oiy, float oiz, float& tmin, float& tmax) {
-#if RT_SLAB_FMA
-    const float x0 = fmaf(lo_x, ix, -oix), x1 = fmaf(hi_x, ix, -oix);
-    const float y0 = fmaf(lo_y, iy, -oiy), y1 = fmaf(hi_y, iy, -oiy);
-    const float z0 = fmaf(lo_z, iz, -oiz), z1 = fmaf(hi_z, iz, -oiz);
-#else
-    const float x0 = (lo_x - ox) * ix, x1 = (hi_x - ox) * ix;
-    const float y0 = (lo_y - oy) * iy, y1 = (hi_y - oy) * iy;
-    const float z0 = (lo_z - oz) * iz, z1 = (hi_z - oz) * iz;
-#endif
+// Slab test of one box against a ray given as inv = 1/d: the reference's (b - o)
+// scaled by 1/d instead of divided by d (MathLib.cl:167-199).
+__device__ __forceinline__ void slab(float lo_x, float hi_x, float lo_y, float hi_y, float lo_z, float hi_z,
+                                     rtm_f3 o, float ix, float iy, float iz, float& tmin, float& tmax) {
+    const float x0 = (lo_x - o.x) * ix, x1 = (hi_x - o.x) * ix;
+    const float y0 = (lo_y - o.y) * iy, y1 = (hi_y - o.y) * iy;
+    const float z0 = (lo_z - o.z) * iz, z1 = (hi_z - o.z) * iz;
     tmin = fmaxf(fmaxf(fminf(x0, x1), fminf(y0, y1)), fminf(z0, z1));
     tmax = fminf(fminf(fmaxf(x0, x1), fmaxf(y0, y1)), fmaxf(z0, z1));
 }
 
+// A box is entered in front of the best hit: tmax >= tmin, tmax >= 0 and tmin <= cull, in one
+// compare for the never-NaN slab values and cull > 0.
+__device__ __forceinline__ bool box_hit(float tmin, float tmax, float cull) {
+    return fmaxf(tmin, 0.0f) <= fminf(tmax, cull);
+}
+
 constexpr float CULL_MARGIN = 1.0f + 0x1p-12f;
-#ifndef RT_HIT3
-#define RT_HIT3 1
-#endif
 
 __device__ __forceinline__ bool mt_vals(float4 g0, float4 g1, float4 g2, rtm_f3 o, rtm_f3 d, float* kout, int* rank);
 
@@ -236,83 +225,17 @@ __device__ __forceinline__ LaneStack lane_stack(const DevScene& S, int* lds_base
     return st;
 }
 
-#if RT_BVH_WIDTH != 4
+// One FAST BVH2 node on its loaded data: a / b = (lo.x hi.x lo.y hi.y) of child 0 / 1, z = (lo.z
+// hi.z) of both, e = the child refs.  Both child boxes are tested; when both are hit the farther is
+// pushed with its entry distance.  Returns the nearer hit child, or INT_MIN when none is hit (pop next).
 template <bool OVF>
 __device__ __forceinline__ int node_pick(float4 a, float4 b, float4 z, int2 e, rtm_f3 o, float ix, float iy,
-                                         float iz, float oix, float oiy, float oiz, float cull, const LaneStack& st,
-                                         unsigned& soff);
-#endif
-
-// One FAST node: test every child box against the ray, push the hit children
-// except the nearest (farthest first, with their entry distance), and return the
-// nearest hit child, or INT_MIN when none is hit (pop next).  np: the node (AoS:
-// kNodeF4 consecutive float4; SOA: float4 planes kstride bytes apart).
-template <bool OVF>
-__device__ __forceinline__ int node_step(const char* np, unsigned kstride, rtm_f3 o, float ix, float iy, float iz,
-                                         float oix, float oiy, float oiz, float cull, const LaneStack& st,
-                                         unsigned& soff) {
-#if RT_BVH_WIDTH == 4
-    const float4 lx = *reinterpret_cast<const float4*>(np);
-    const float4 hx = *reinterpret_cast<const float4*>(np + kstride);
-    const float4 ly = *reinterpret_cast<const float4*>(np + 2 * kstride);
-    const float4 hy = *reinterpret_cast<const float4*>(np + 3 * kstride);
-    const float4 lz = *reinterpret_cast<const float4*>(np + 4 * kstride);
-    const float4 hz = *reinterpret_cast<const float4*>(np + 5 * kstride);
-    const int4 rf = *reinterpret_cast<const int4*>(np + 6 * kstride);
-    const float alx[4] = {lx.x, lx.y, lx.z, lx.w}, ahx[4] = {hx.x, hx.y, hx.z, hx.w};
-    const float aly[4] = {ly.x, ly.y, ly.z, ly.w}, ahy[4] = {hy.x, hy.y, hy.z, hy.w};
-    const float alz[4] = {lz.x, lz.y, lz.z, lz.w}, ahz[4] = {hz.x, hz.y, hz.z, hz.w};
-    float t[4];
-    int r[4] = {rf.x, rf.y, rf.z, rf.w};
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        float tn, tx;
-        slab_fma(alx[i], ahx[i], aly[i], ahy[i], alz[i], ahz[i], o.x, o.y, o.z, ix, iy, iz, oix, oiy, oiz, tn, tx);
-        t[i] = fmaxf(tn, 0.0f) <= fminf(tx, cull) ? tn : INFINITY;   // misses sort last
-    }
-    auto ce = [&](int a, int b) __attribute__((always_inline)) {
-        const bool sw = t[b] < t[a];
-        const float ta = t[a], tb = t[b];
-        const int ra = r[a], rb = r[b];
-        t[a] = sw ? tb : ta; t[b] = sw ? ta : tb;
-        r[a] = sw ? rb : ra; r[b] = sw ? ra : rb;
-    };
-    ce(0, 1); ce(2, 3); ce(0, 2); ce(1, 3); ce(1, 2);
-#pragma unroll
-    for (int i = 3; i >= 1; --i) {
-        if (t[i] < INFINITY) {
-            st.template put<OVF>(soff, make_int2(r[i], __float_as_int(t[i])));
-            soff += st.stride;
-        }
-    }
-    return t[0] < INFINITY ? r[0] : INT_MIN;
-#else
-    const float4 a = *reinterpret_cast<const float4*>(np);
-    const float4 b = *reinterpret_cast<const float4*>(np + kstride);
-    const float4 z = *reinterpret_cast<const float4*>(np + 2 * kstride);
-    const int2 e = *reinterpret_cast<const int2*>(np + 3 * kstride);
-    return node_pick<OVF>(a, b, z, e, o, ix, iy, iz, oix, oiy, oiz, cull, st, soff);
-#endif
-}
-
-#if RT_BVH_WIDTH != 4
-// The BVH2 node step on a loaded node: a / b = (lo.x hi.x lo.y hi.y) of child 0 / 1, z = (lo.z hi.z)
-// of both, e = the child refs.
-template <bool OVF>
-__device__ __forceinline__ int node_pick(float4 a, float4 b, float4 z, int2 e, rtm_f3 o, float ix, float iy,
-                                         float iz, float oix, float oiy, float oiz, float cull, const LaneStack& st,
-                                         unsigned& soff) {
+                                         float iz, float cull, const LaneStack& st, unsigned& soff) {
     float t0n, t0x, t1n, t1x;
-    slab_fma(a.x, a.y, a.z, a.w, z.x, z.y, o.x, o.y, o.z, ix, iy, iz, oix, oiy, oiz, t0n, t0x);
-    slab_fma(b.x, b.y, b.z, b.w, z.z, z.w, o.x, o.y, o.z, ix, iy, iz, oix, oiy, oiz, t1n, t1x);
-#if RT_HIT3
-    // t0x >= t0n && t0x >= 0 && t0n <= cull, for the never-NaN slab values and cull > 0
-    const bool h0 = fmaxf(t0n, 0.0f) <= fminf(t0x, cull);
-    const bool h1 = fmaxf(t1n, 0.0f) <= fminf(t1x, cull);
-#else
-    const bool h0 = t0x >= t0n && t0x >= 0.0f && t0n <= cull;
-    const bool h1 = t1x >= t1n && t1x >= 0.0f && t1n <= cull;
-#endif
+    slab(a.x, a.y, a.z, a.w, z.x, z.y, o, ix, iy, iz, t0n, t0x);
+    slab(b.x, b.y, b.z, b.w, z.z, z.w, o, ix, iy, iz, t1n, t1x);
+    const bool h0 = box_hit(t0n, t0x, cull);
+    const bool h1 = box_hit(t1n, t1x, cull);
     if (h0 && h1) {
         const bool first0 = t0n <= t1n;
         st.template put<OVF>(soff, make_int2(first0 ? e.y : e.x, __float_as_int(first0 ? t1n : t0n)));
@@ -322,7 +245,17 @@ __device__ __forceinline__ int node_pick(float4 a, float4 b, float4 z, int2 e, r
     if (h0 || h1) return h0 ? e.x : e.y;
     return INT_MIN;
 }
-#endif
+
+// node_pick on node np (AoS: 4 consecutive float4; SOA: float4 planes kstride bytes apart).
+template <bool OVF>
+__device__ __forceinline__ int node_step(const char* np, unsigned kstride, rtm_f3 o, float ix, float iy, float iz,
+                                         float cull, const LaneStack& st, unsigned& soff) {
+    const float4 a = *reinterpret_cast<const float4*>(np);
+    const float4 b = *reinterpret_cast<const float4*>(np + kstride);
+    const float4 z = *reinterpret_cast<const float4*>(np + 2 * kstride);
+    const int2 e = *reinterpret_cast<const int2*>(np + 3 * kstride);
+    return node_pick<OVF>(a, b, z, e, o, ix, iy, iz, cull, st, soff);
+}
 
 // One item per iteration: an internal node (both child boxes tested, nearer hit
 // child continues, the farther is pushed with its entry distance) or a leaf
@@ -345,10 +278,9 @@ __device__ Hit trace_fast(const DevScene& S, const float4* __restrict__ nodes, c
     // 16 lanes reading 16 different nodes hit 16 different bank groups
     const unsigned kstride = SOA ? 16u * (unsigned)S.nnodes : 16u;
     const float ix = 1.0f / d.x, iy = 1.0f / d.y, iz = 1.0f / d.z;
-    const float oix = o.x * ix, oiy = o.y * iy, oiz = o.z * iz;
     float tmin, tmax;
-    slab_fma(S.root_box[0], S.root_box[3], S.root_box[1], S.root_box[4], S.root_box[2], S.root_box[5], o.x, o.y, o.z,
-             ix, iy, iz, oix, oiy, oiz, tmin, tmax);
+    slab(S.root_box[0], S.root_box[3], S.root_box[1], S.root_box[4], S.root_box[2], S.root_box[5], o, ix, iy, iz,
+         tmin, tmax);
     if (!(tmax >= tmin && tmax >= 0.0f)) return best;
     int item = S.root_ref;
     unsigned soff = 0;
@@ -357,7 +289,7 @@ __device__ Hit trace_fast(const DevScene& S, const float4* __restrict__ nodes, c
         if (item >= 0) {
             if (COUNT) c.nodes++;
             const char* np = nb + (SOA ? 16u : 16u * kNodeF4) * (unsigned)item;
-            const int next = node_step<OVF>(np, kstride, o, ix, iy, iz, oix, oiy, oiz, best.k * CULL_MARGIN, st, soff);
+            const int next = node_step<OVF>(np, kstride, o, ix, iy, iz, best.k * CULL_MARGIN, st, soff);
             if (next != INT_MIN) {
                 item = next;
                 continue;
@@ -391,13 +323,11 @@ __device__ Hit trace_fast(const DevScene& S, const float4* __restrict__ nodes, c
     return best;
 }
 
-// Scenes of at most RT_BRUTE_MAX triangles: every lane of the wave tests the
-// same triangle at the same time, its record read once per wave through scalar
-// loads (SGPR operands, no LDS, no stack, no divergence).  The set of accepted
-// triangles is FAST's (own leaf box passes with the same slab arithmetic, MT
-// hit, k > 1e-4), and records are in the reference's DFS order, so the strict
-// `<` keeps the lowest rank on equal distances: the same hit as trace_fast.
-// Record (4 x float4): lo.xyz hi.x | hi.yz a.xy | a.z e1.xyz | e2.xyz tri.
+// Small scenes (brute_max): every lane of the wave tests the same leaf box at the same time, its
+// record read once per wave through scalar loads (SGPR operands, no LDS, no stack, no divergence).
+// The set of accepted triangles is FAST's (own leaf box passes with the same slab arithmetic, MT
+// hit, k > 1e-4), and records are in the reference's DFS order, so the lowest rank wins on equal
+// distances: the same hit as trace_fast.
 // Read-only data read through the constant address space: wave-uniform addresses become scalar
 // loads (s_load_*) whatever the surrounding control flow.
 typedef const float __attribute__((address_space(4))) const_f;
@@ -418,48 +348,10 @@ __device__ __forceinline__ float4 sgpr4(float4 v) {
     return make_float4(sgpr1(v.x), sgpr1(v.y), sgpr1(v.z), sgpr1(v.w));
 }
 
-template <bool COUNT>
-__device__ Hit trace_brute(const DevScene& S, rtm_f3 o, rtm_f3 d, Cnt& c) {
-    Hit best{1000.0f, -1};
-    if (COUNT) c.rays++;
-    const float ix = 1.0f / d.x, iy = 1.0f / d.y, iz = 1.0f / d.z;
-    const float oix = o.x * ix, oiy = o.y * iy, oiz = o.z * iz;
-    for (int q = 0; q < S.nbrute; ++q) {
-        if (COUNT) count_wave(c.wave_trav);
-        // the record is wave-uniform: readfirstlane pins it in SGPRs (one s_load_dwordx16, SGPR
-        // operands).  Prefetching the next record costs more SALU moves than the latency it hides.
-        const ConstF4 cb = as_const(S.brute);
-        const float4 r0 = sgpr4(cb[4 * q + 0]), r1 = sgpr4(cb[4 * q + 1]);
-        const float4 r2 = sgpr4(cb[4 * q + 2]), r3 = sgpr4(cb[4 * q + 3]);
-        float tn, tx;
-        slab_fma(r0.x, r0.w, r0.y, r1.x, r0.z, r1.y, o.x, o.y, o.z, ix, iy, iz, oix, oiy, oiz, tn, tx);
-        const bool pass = fmaxf(tn, 0.0f) <= fminf(tx, best.k * CULL_MARGIN);
-        if (COUNT) c.nodes++;
-        if (__ballot(pass) == 0) continue;   // wave-uniform: nobody's box is hit
-        if (COUNT && pass) c.tris++;
-        const rtm_f3 a = rtm_v3(r1.z, r1.w, r2.x), e1 = rtm_v3(r2.y, r2.z, r2.w), e2 = rtm_v3(r3.x, r3.y, r3.z);
-        const rtm_f3 h = rtm_cross(d, e2);
-        const float det = rtm_dot(e1, h);
-        const float f = 1.0f / det;
-        const rtm_f3 sv = rtm_sub(o, a);
-        const float u = f * rtm_dot(sv, h);
-        const rtm_f3 qv = rtm_cross(sv, e1);
-        const float v = f * rtm_dot(d, qv);
-        const float k = f * rtm_dot(e2, qv);
-        const bool parallel = det > -0.0000001f && det < 0.0000001f;
-        const bool hit = !parallel && !(u < 0.0f || u > 1.0f) && !(v < 0.0f || u + v > 1.0f) && (k > 0.0000001f);
-        if (pass && hit && k > 0.0001f && k < best.k) {
-            best.k = k;
-            best.tri = __float_as_int(r3.w);
-        }
-    }
-    return best;
-}
-
-// Brute force with ray-triangle pair compaction.  The lock-step loop above runs
-// the Moller-Trumbore block for the whole wave whenever any lane's box passes:
-// on C2 that is 28 of 36 triangles per ray round, at ~6 passing lanes each.
-// Here the box tests stay lock-step (scalar records), but every passing
+// Brute force with ray-triangle pair compaction.  Running the Moller-Trumbore block
+// for the whole wave whenever any lane's box passes would run it for 28 of C2's 36
+// triangles per ray round at ~6 passing lanes each.  The box tests stay lock-step
+// (scalar records), but every passing
 // (lane, triangle) pair is appended to a per-wave LDS queue; whenever the queue
 // holds a full wave of pairs, each lane takes one pair -- the owner's ray from
 // an LDS table, the triangle record by a vector load -- runs the same MT test
@@ -500,7 +392,6 @@ __device__ Hit trace_brute_compact(const DevScene& S, rtm_f3 o, rtm_f3 d, char* 
     bestk[lane] = nokey;
     wave_lds_sync();
     const float ix = 1.0f / d.x, iy = 1.0f / d.y, iz = 1.0f / d.z;
-    const float oix = o.x * ix, oiy = o.y * iy, oiz = o.z * iz;
     float bk = 1000.0f;
     unsigned head = 0, tail = 0;   // wave-uniform ring positions
     auto run_batch = [&](int n) __attribute__((always_inline)) {
@@ -564,9 +455,9 @@ __device__ Hit trace_brute_compact(const DevScene& S, rtm_f3 o, rtm_f3 d, char* 
 #pragma unroll
             for (int j = 0; j < kBoxGroup; ++j) {
                 float tn, tx;
-                slab_fma(bx[2 * j].x, bx[2 * j].y, bx[2 * j].z, bx[2 * j].w, bx[2 * j + 1].x, bx[2 * j + 1].y, o.x,
-                         o.y, o.z, ix, iy, iz, oix, oiy, oiz, tn, tx);
-                pass[j] = fmaxf(tn, 0.0f) <= fminf(tx, cull);
+                slab(bx[2 * j].x, bx[2 * j].y, bx[2 * j].z, bx[2 * j].w, bx[2 * j + 1].x, bx[2 * j + 1].y, o, ix, iy,
+                     iz, tn, tx);
+                pass[j] = box_hit(tn, tx, cull);
             }
 #pragma unroll
             for (int j = 0; j < kBoxGroup; ++j) {
@@ -591,8 +482,8 @@ __device__ Hit trace_brute_compact(const DevScene& S, rtm_f3 o, rtm_f3 d, char* 
             if (g < S.nbox) {
                 const float4 b0 = boxrec[2 * g], b1 = boxrec[2 * g + 1];
                 float tn, tx;
-                slab_fma(b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, o.x, o.y, o.z, ix, iy, iz, oix, oiy, oiz, tn, tx);
-                pass = fmaxf(tn, 0.0f) <= fminf(tx, bk * CULL_MARGIN);
+                slab(b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, o, ix, iy, iz, tn, tx);
+                pass = box_hit(tn, tx, bk * CULL_MARGIN);
                 qa = __float_as_int(b1.z);
                 qb = __float_as_int(b1.w);
                 if (COUNT) c.nodes += qb >= 0 ? 2 : 1;
@@ -612,13 +503,6 @@ __device__ Hit trace_brute_compact(const DevScene& S, rtm_f3 o, rtm_f3 d, char* 
     return best;
 }
 
-#ifndef RT_BRUTE_COMPACT
-#define RT_BRUTE_COMPACT 1
-#endif
-#ifndef RT_BRUTE_LDS
-#define RT_BRUTE_LDS 1   // MT batches read the triangle records from an LDS copy (48 B stride)
-#endif
-
 // stk/B: the REF traversal's int stack in LDS; st: the FAST traversal's stack.
 // mtrec/mtstride: where the brute-force MT batches read triangle records (float4 units).
 // BLDS: the caller staged the MT records in LDS at mtrec (3 float4 per triangle); otherwise they
@@ -628,14 +512,10 @@ __device__ __forceinline__ Hit trace(const DevScene& S, const float4* nodes, con
                                      int* stk, int B, const LaneStack& st, Cnt& c, const float4* mtrec = nullptr,
                                      int ts = 1, const float4* boxrec = nullptr) {
     if (TRAV == TRAV_REF) return trace_ref<COUNT>(S, o, d, stk, B, c);
-    if (S.nbrute > 0) {
-        if (RT_BRUTE_COMPACT)
-            return trace_brute_compact<COUNT>(S, o, d, reinterpret_cast<char*>(stk - threadIdx.x) +
-                                                            (threadIdx.x >> 6) * BRUTE_WAVE_LDS,
-                                              BLDS ? mtrec : S.brute + 1, BLDS ? 3u : 4u, c, BLDS ? ts : 1,
-                                              boxrec);
-        return trace_brute<COUNT>(S, o, d, c);
-    }
+    if (S.nbrute > 0)
+        return trace_brute_compact<COUNT>(S, o, d, reinterpret_cast<char*>(stk - threadIdx.x) +
+                                                        (threadIdx.x >> 6) * BRUTE_WAVE_LDS,
+                                          BLDS ? mtrec : S.brute + 1, BLDS ? 3u : 4u, c, BLDS ? ts : 1, boxrec);
     return trace_fast<COUNT, SOA, OVF>(S, nodes, tris, o, d, st, c);
 }
 
@@ -844,82 +724,70 @@ __device__ __forceinline__ void log_event(const FrameParams& F, float kind, int 
     *F.log_count = n + 1;
 }
 
-// Mean + clamp of one pixel (Raytracing.cl:211-220).  RT_NT_STORE: write the
-// frame with nontemporal stores (it is written once and never re-read).
-#ifndef RT_NT_STORE
-#define RT_NT_STORE 0
-#endif
+// Mean + clamp of one pixel (Raytracing.cl:211-220).
 __device__ __forceinline__ void store_pixel(float* __restrict__ out, int p, rtm_f3 acc, int spp) {
     const rtm_f3 o = rtm_div(acc, (float)spp);
     float* dst = out + 3 * (int64_t)p;
-#if RT_NT_STORE
-    __builtin_nontemporal_store(rtm_fmax(rtm_fmin(o.x, 1.0f), 0.0f), dst);
-    __builtin_nontemporal_store(rtm_fmax(rtm_fmin(o.y, 1.0f), 0.0f), dst + 1);
-    __builtin_nontemporal_store(rtm_fmax(rtm_fmin(o.z, 1.0f), 0.0f), dst + 2);
-#else
     dst[0] = rtm_fmax(rtm_fmin(o.x, 1.0f), 0.0f);
     dst[1] = rtm_fmax(rtm_fmin(o.y, 1.0f), 0.0f);
     dst[2] = rtm_fmax(rtm_fmin(o.z, 1.0f), 0.0f);
-#endif
 }
 
 enum Phase { FETCH = 0, PRIMARY = 1, PREP = 2, BOUNCE = 3, SUN = 4, DONE = 5 };
 
 // ---- pixel hand-out ----
-// A wave keeps a private range [next, end) of tile pixels and refills it from the global counter
-// (one device-scope atomic on an address every wave of every XCD shares) only when it runs short;
-// the base comes back as a scalar, and once the counter is exhausted (`dry`) the wave never goes
-// back to it.  RT_FETCH_CHUNK > 1 reserves that many pixels per atomic; measured on C2 (1 GPU),
-// 1 is fastest (9.9 ms against 10.3-10.6 ms for 2..16: reserved pixels unbalance the end of the
-// frame).  All state is wave-uniform.  rank: the requesting lane's (or team's) rank in `need`;
-// returns its tile pixel index (>= nloc: none left).
-#ifndef RT_FETCH_CHUNK
-#define RT_FETCH_CHUNK 1
-#endif
+// Tile pixels are dealt in chunks of 2^kChunkShift consecutive pixels: chunk c belongs to group
+// c % kGroups.  A block of group g = blockIdx.x % kGroups (under the round-robin dispatch of blocks
+// over the 8 XCDs, the blocks of one XCD) takes pixels from group g's counter, one device-scope
+// atomic per wave refill, so every 128-byte line of the frame is written through one XCD's L2 (a
+// line written from several L2s leaves each of them as a partial write).  A group whose pixels are
+// exhausted steals from the next groups in turn; `dry` remembers (per wave) which are exhausted.
+// Correctness does not depend on the placement: every pixel is taken exactly once whatever XCD a
+// block runs on.
 struct PixelQueue {
-    unsigned next = 0, end = 0;
-    bool dry = false;   // the global counter is exhausted
+    unsigned dry = 0;   // bit g: group g's counter is exhausted
 };
-__device__ __forceinline__ unsigned take_pixel(PixelQueue& Q, unsigned long long need, unsigned rank,
-                                               unsigned* __restrict__ counter, unsigned nloc, int lane) {
-    const unsigned k = (unsigned)__popcll(need);
-    const unsigned avail = Q.end - Q.next;
-    if (k <= avail) {
-        const unsigned q = Q.next + rank;
-        Q.next += k;
-        return q;
-    }
-    if (Q.dry) {
-        const unsigned q = rank < avail ? Q.next + rank : nloc;
-        Q.next = Q.end;
-        return q;
-    }
-    const unsigned want = max(k - avail, (unsigned)RT_FETCH_CHUNK);
+
+// group g's j-th pixel (chunks g, g + kGroups, g + 2 kGroups, ...: increasing in j)
+__device__ __forceinline__ unsigned group_pixel(unsigned g, unsigned j) {
+    constexpr unsigned m = (1u << kChunkShift) - 1u;
+    return (((j >> kChunkShift) * (unsigned)kGroups + g) << kChunkShift) | (j & m);
+}
+
+// pixels of group g in a tile of nloc pixels (wave-uniform)
+__device__ __forceinline__ unsigned group_pixels(unsigned g, unsigned nloc) {
+    const unsigned chunks = nloc >> kChunkShift, rem = nloc & ((1u << kChunkShift) - 1u);
+    const unsigned full = chunks > g ? (chunks - 1u - g) / (unsigned)kGroups + 1u : 0u;
+    return (full << kChunkShift) + (chunks % (unsigned)kGroups == g ? rem : 0u);
+}
+
+// need: wave-uniform mask of the requesting lanes (team leaders); lane0: the calling lane's team
+// leader.  Returns the calling lane's tile pixel index (>= nloc: none left in the tile).  Called
+// with the whole wave active; all control flow is wave-uniform, and the requests are served in
+// rank order (group by group), so a lane only needs its rank.
+__device__ __forceinline__ unsigned take_pixel(PixelQueue& Q, unsigned long long need, int lane0,
+                                               unsigned* __restrict__ counters, unsigned nloc, int lane) {
+    const bool mine = (need >> lane0) & 1ull;
+    const unsigned rank = (unsigned)__popcll(need & ((1ull << lane0) - 1ull));
+    const unsigned total = (unsigned)__popcll(need);
     const int leader = __ffsll((long long)need) - 1;
-    unsigned got = 0;
-    if (lane == leader) got = atomicAdd(counter, want);
-    const unsigned nb = (unsigned)__builtin_amdgcn_readfirstlane((int)__shfl(got, leader, 64));
-    const unsigned q = rank < avail ? Q.next + rank : nb + (rank - avail);
-    if (nb >= nloc) {
-        Q.next = Q.end;
-        Q.dry = true;
-    } else {
-        Q.end = min(nb + want, nloc);
-        Q.next = min(nb + (k - avail), Q.end);
-        Q.dry = nb + want >= nloc;
+    unsigned q = nloc;
+    unsigned base = 0;   // requests served so far
+    unsigned g = blockIdx.x % (unsigned)kGroups;
+    for (int t = 0; t < kGroups && base < total; ++t, g = (g + 1u) % (unsigned)kGroups) {
+        if ((Q.dry >> g) & 1u) continue;
+        const unsigned k = total - base;
+        unsigned got = 0;
+        if (lane == leader) got = atomicAdd(counters + g * (unsigned)(kCounterStride / 4), k);
+        const unsigned j0 = (unsigned)__builtin_amdgcn_readfirstlane((int)__shfl(got, leader, 64));
+        const unsigned have = group_pixels(g, nloc);
+        const unsigned nok = j0 < have ? min(have - j0, k) : 0u;
+        if (mine && rank >= base && rank < base + nok) q = group_pixel(g, j0 + (rank - base));
+        if (nok < k) Q.dry |= 1u << g;   // the group's sequence has run past the tile
+        base += nok;
     }
     return q;
 }
-
-// RT_MIN_WAVES: waves per SIMD the register allocator must leave room for (0 = compiler's choice).
-#ifndef RT_MIN_WAVES
-#define RT_MIN_WAVES 0
-#endif
-#if RT_MIN_WAVES > 0
-#define RT_RENDER_BOUNDS __launch_bounds__(256, RT_MIN_WAVES)
-#else
-#define RT_RENDER_BOUNDS __launch_bounds__(256)
-#endif
 
 // One persistent lane = one pixel at a time.  Lanes that finish their pixel
 // take the next pixel index from a global counter: the wave ballots the lanes
@@ -928,7 +796,10 @@ __device__ __forceinline__ unsigned take_pixel(PixelQueue& Q, unsigned long long
 // rest of its wave finishes a slower pixel.  Per loop iteration every busy
 // lane traces exactly one ray (primary, bounce or sun ray).
 template <int TRAV, bool COUNT, bool LOG = false, bool SMEM = false, bool OVF = false, int BRUTE = 0>
-__global__ void RT_RENDER_BOUNDS render_kernel(DevScene S, FrameParams F, float* __restrict__ out,
+// amdgpu_waves_per_eu(5): the register allocator keeps the kernel at 96 VGPRs, i.e. 5 waves per SIMD
+// (one register more costs a wave per SIMD and ~10 % on C2); the product instantiations fit without
+// spills, the instrumented (COUNT) ones spill a few registers to scratch.
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) render_kernel(DevScene S, FrameParams F, float* __restrict__ out,
                                                unsigned long long* __restrict__ counts,
                                                unsigned int* __restrict__ work_counter,
                                                const LaunchConst* __restrict__ lconst) {
@@ -1011,8 +882,7 @@ __global__ void RT_RENDER_BOUNDS render_kernel(DevScene S, FrameParams F, float*
         // teams (BRUTE, F.team lanes per pixel): one bit per team, the team's lanes take the same pixel
         const unsigned long long need = __ballot(phase == FETCH) & team_leaders;
         if (need) {
-            const unsigned rank = (unsigned)__popcll(need & ((1ull << team_lane0) - 1ull));
-            const unsigned int q = take_pixel(pq, need, rank, work_counter, nloc, lane);
+            const unsigned int q = take_pixel(pq, need, team_lane0, work_counter, nloc, lane);
             if (phase == FETCH) {
                 bool ok = q < nloc;
                 if (ok) {
@@ -1214,8 +1084,8 @@ __device__ __forceinline__ bool fast_init(const DevScene& S, FastRay& R, rtm_f3 
     R.iy = 1.0f / d.y;
     R.iz = 1.0f / d.z;
     float tmin, tmax;
-    slab_fma(S.root_box[0], S.root_box[3], S.root_box[1], S.root_box[4], S.root_box[2], S.root_box[5], o.x, o.y, o.z,
-             R.ix, R.iy, R.iz, o.x * R.ix, o.y * R.iy, o.z * R.iz, tmin, tmax);
+    slab(S.root_box[0], S.root_box[3], S.root_box[1], S.root_box[4], S.root_box[2], S.root_box[5], o, R.ix, R.iy, R.iz,
+         tmin, tmax);
     if (!(tmax >= tmin && tmax >= 0.0f)) return true;
     R.item = S.root_ref;
     return false;
@@ -1228,11 +1098,10 @@ template <bool COUNT, bool SOA, bool OVF>
 __device__ __forceinline__ bool fast_round(const DevScene& S, FastRay& R, const char* nb, const char* tb,
                                            const LaneStack& st, unsigned kstride, Cnt& c) {
     const unsigned sstride = st.stride;
-    const float oix = R.o.x * R.ix, oiy = R.o.y * R.iy, oiz = R.o.z * R.iz;
     while (R.item >= 0) {
         if (COUNT) { count_wave(c.wave_trav); c.nodes++; }
         const char* np = nb + (SOA ? 16u : 16u * kNodeF4) * (unsigned)R.item;
-        R.item = node_step<OVF>(np, kstride, R.o, R.ix, R.iy, R.iz, oix, oiy, oiz, R.bk * CULL_MARGIN, st, R.soff);
+        R.item = node_step<OVF>(np, kstride, R.o, R.ix, R.iy, R.iz, R.bk * CULL_MARGIN, st, R.soff);
     }
     if (R.item != INT_MIN) {      // a leaf: one triangle test
         if (COUNT) { count_wave(c.wave_trav); c.tris++; }
@@ -1259,46 +1128,27 @@ __device__ __forceinline__ bool fast_round(const DevScene& S, FastRay& R, const 
     return true;
 }
 
-// One item of trace_fast's loop per call (RT_STEP_UNIFIED): an internal node or a leaf, then a pop
-// when the item yields no next item.  The per-lane sequence of node steps, leaf tests and pops is
-// trace_fast's, so the hit is the same.  Every tracing lane fetches its item with the SAME four
-// vector loads, whether it is a node (64 B: both child boxes + refs) or a triangle (48 B: a.p | rank,
-// e1, e2; the fourth load re-reads its first bytes), so a wave issues 4 load instructions per step
-// with all its tracing lanes active.  On C3 the texture address unit was 89 % busy with the
-// descend-until-leaf rounds of fast_round, whose loads ran with few lanes active.
-// Returns true when the ray is finished.
-// 4 low bits of each of six floats -> a 24-bit child ref (DevScene::nodes48)
-__device__ __forceinline__ int nib6(float a, float b, float c, float d, float e, float f) {
-    return (int)((__float_as_uint(a) & 15u) | ((__float_as_uint(b) & 15u) << 4) | ((__float_as_uint(c) & 15u) << 8) |
-                 ((__float_as_uint(d) & 15u) << 12) | ((__float_as_uint(e) & 15u) << 16) |
-                 ((__float_as_uint(f) & 15u) << 20));
-}
-
-// COMPACT: nb / tb are DevScene::nodes48 / tri2 -- a node is 48 bytes, so an item takes three loads.
-template <bool COUNT, bool SOA, bool OVF, bool COMPACT = false>
+// One item of trace_fast's loop per call: an internal node or a leaf, then a pop when the item
+// yields no next item.  The per-lane sequence of node steps, leaf tests and pops is trace_fast's, so
+// the hit is the same.  Every tracing lane fetches its item with the SAME four vector loads, whether
+// it is a node (64 B: both child boxes + refs) or a triangle (48 B: a.p | rank, e1, e2; the fourth
+// load re-reads its first bytes), so a wave issues 4 load instructions per step with all its
+// tracing lanes active.  On C3 the texture address unit was 89 % busy with the descend-until-leaf
+// rounds of fast_round, whose loads ran with few lanes active.  Returns true when the ray is finished.
+template <bool COUNT, bool SOA, bool OVF>
 __device__ __forceinline__ bool fast_step(const DevScene& S, FastRay& R, const char* nb, const char* tb,
                                           const LaneStack& st, unsigned kstride, Cnt& c) {
-#if RT_BVH_WIDTH != 4
     const bool node = R.item >= 0;
-    const char* p = COMPACT ? (node ? nb + (unsigned)kCompactStride * ((unsigned)R.item >> 2) : tb + ~(unsigned)R.item)
-                            : (node ? nb + (SOA ? 16u : 16u * kNodeF4) * (unsigned)R.item : tb + ~(unsigned)R.item);
-    const unsigned ks = (COMPACT || !node) ? 16u : kstride;
+    const char* p = node ? nb + (SOA ? 16u : 16u * kNodeF4) * (unsigned)R.item : tb + ~(unsigned)R.item;
+    const unsigned ks = node ? kstride : 16u;
     const float4 g0 = *reinterpret_cast<const float4*>(p);
     const float4 g1 = *reinterpret_cast<const float4*>(p + ks);
     const float4 g2 = *reinterpret_cast<const float4*>(p + 2 * ks);
-    int2 e = make_int2(0, 0);
-    if (!COMPACT) e = *reinterpret_cast<const int2*>(p + (node ? 3 * ks : 0u));
+    const int2 e = *reinterpret_cast<const int2*>(p + (node ? 3 * ks : 0u));
     if (COUNT) count_wave(c.wave_trav);
     if (node) {
         if (COUNT) c.nodes++;
-        if (COMPACT) {
-            const unsigned x = (unsigned)R.item >> 2, ty = (unsigned)R.item & 3u;
-            constexpr unsigned cs = (unsigned)kCompactStride;
-            e.x = (ty & 1u) ? (int)~(2u * cs * x) : nib6(g0.x, g0.y, g0.z, g0.w, g2.x, g2.y);
-            e.y = (ty & 2u) ? (int)~(2u * cs * x + cs) : nib6(g1.x, g1.y, g1.z, g1.w, g2.z, g2.w);
-        }
-        const float oix = R.o.x * R.ix, oiy = R.o.y * R.iy, oiz = R.o.z * R.iz;
-        R.item = node_pick<OVF>(g0, g1, g2, e, R.o, R.ix, R.iy, R.iz, oix, oiy, oiz, R.bk * CULL_MARGIN, st, R.soff);
+        R.item = node_pick<OVF>(g0, g1, g2, e, R.o, R.ix, R.iy, R.iz, R.bk * CULL_MARGIN, st, R.soff);
         if (R.item != INT_MIN) return false;
     } else {
         if (COUNT) c.tris++;
@@ -1320,30 +1170,16 @@ __device__ __forceinline__ bool fast_step(const DevScene& S, FastRay& R, const c
         }
     }
     return true;
-#else
-    return fast_round<COUNT, SOA, OVF>(S, R, nb, tb, st, kstride, c);
-#endif
 }
 
 // FrameParams::step = 0 (auto): one item per step (fast_step) when the node array is at most this
 // many bytes (L2-resident scenes, bound by the texture-address unit), descend-until-leaf rounds
 // (fast_round) above (C5's 64 MB: bound by the latency of L2 misses; fast_round 1000 vs fast_step
 // 944 Msamples/s there)
-#ifndef RT_STEP_MAX_BYTES
-#define RT_STEP_MAX_BYTES (16u << 20)
-#endif
+constexpr size_t kStepMaxBytes = 16u << 20;
 
-#ifndef RT_RESUME_MIN_WAVES
-#define RT_RESUME_MIN_WAVES 0
-#endif
-#if RT_RESUME_MIN_WAVES > 0
-#define RT_RESUME_BOUNDS __launch_bounds__(256, RT_RESUME_MIN_WAVES)
-#else
-#define RT_RESUME_BOUNDS __launch_bounds__(256)
-#endif
-
-template <bool COUNT, bool LOG, bool SMEM, bool OVF, bool STEP, bool COMPACT>
-__global__ void RT_RESUME_BOUNDS render_resume_kernel(DevScene S, FrameParams F, float* __restrict__ out,
+template <bool COUNT, bool LOG, bool SMEM, bool OVF, bool STEP>
+__global__ void __launch_bounds__(256) render_resume_kernel(DevScene S, FrameParams F, float* __restrict__ out,
                                                       unsigned long long* __restrict__ counts,
                                                       unsigned int* __restrict__ work_counter,
                                                       const LaunchConst* __restrict__ lconst) {
@@ -1366,8 +1202,6 @@ __global__ void RT_RESUME_BOUNDS render_resume_kernel(DevScene S, FrameParams F,
     const LaneStack lst = lane_stack(S, lds_stack);
     const char* const nb = reinterpret_cast<const char*>(nodes);
     const char* const tb = reinterpret_cast<const char*>(tris);
-    const char* const nb48 = reinterpret_cast<const char*>(S.nodes48);   // COMPACT item steps
-    const char* const tb2 = reinterpret_cast<const char*>(S.tri2);
     const unsigned kstride = SMEM ? 16u * (unsigned)S.nnodes : 16u;
     const int W = F.width;
     const int imgSize = (int)F.npix;
@@ -1412,7 +1246,6 @@ __global__ void RT_RESUME_BOUNDS render_resume_kernel(DevScene S, FrameParams F,
     };
     auto start = [&](rtm_f3 o, rtm_f3 d) __attribute__((always_inline)) {
         tracing = !fast_init<COUNT>(S, T, o, d, c);
-        if (COMPACT) T.item = S.root_ref48;
         T.any = false;
     };
 
@@ -1421,8 +1254,7 @@ __global__ void RT_RESUME_BOUNDS render_resume_kernel(DevScene S, FrameParams F,
         // -- refill: ballot the lanes that need a pixel, one atomic per wave --
         const unsigned long long need = __ballot(phase == FETCH);
         if (need) {
-            const unsigned rank = (unsigned)__popcll(need & ((1ull << lane) - 1ull));
-            const unsigned int q = take_pixel(pq, need, rank, work_counter, nloc, lane);
+            const unsigned int q = take_pixel(pq, need, lane, work_counter, nloc, lane);
             if (phase == FETCH) {
                 bool ok = q < nloc;
                 if (ok) {
@@ -1561,8 +1393,7 @@ __global__ void RT_RESUME_BOUNDS render_resume_kernel(DevScene S, FrameParams F,
             if (lane == 0) c.cyc_shade += t_mid - t_iter;
         }
         while (true) {
-            if (tracing && (STEP ? fast_step<COUNT, SMEM, OVF, COMPACT>(S, T, COMPACT ? nb48 : nb, COMPACT ? tb2 : tb,
-                                                                         lst, kstride, c)
+            if (tracing && (STEP ? fast_step<COUNT, SMEM, OVF>(S, T, nb, tb, lst, kstride, c)
                                  : fast_round<COUNT, SMEM, OVF>(S, T, nb, tb, lst, kstride, c)))
                 tracing = false;
             const unsigned long long tr = __ballot(tracing);
@@ -1617,14 +1448,13 @@ __global__ void rgb8_kernel(const float* __restrict__ in, uint8_t* __restrict__ 
 }
 
 template <int TRAV, bool COUNT, bool LOG, bool SMEM = false, bool RESUME = false, bool OVF = false,
-          bool BRUTE = false, bool STEP = true, bool COMPACT = false>
+          bool BRUTE = false, bool STEP = true>
 hipError_t launch_t(const DevScene& sc, const FrameParams& fp, int block, float* d_out, unsigned long long* d_counts,
                     unsigned int* d_work, hipStream_t stream) {
     // FAST: int2 entries; the brute-force path of small scenes needs no stack
     const int depth = (TRAV == TRAV_REF) ? REF_STACK : (sc.nbrute > 0 ? 1 : 2 * (sc.stack_lds > 0 ? sc.stack_lds : 1));
     size_t lds = (size_t)depth * block * sizeof(int);
-    if (TRAV == TRAV_FAST && sc.nbrute > 0 && RT_BRUTE_COMPACT)
-        lds = std::max(lds, (size_t)(block / 64) * BRUTE_WAVE_LDS);
+    if (TRAV == TRAV_FAST && sc.nbrute > 0) lds = std::max(lds, (size_t)(block / 64) * BRUTE_WAVE_LDS);
     if (BRUTE)
         lds = (size_t)(block / 64) * BRUTE_WAVE_LDS + (size_t)sc.nbrute * 48 + (size_t)sc.nbox * 32 +
               (size_t)sc.ntri * 64 + (size_t)sc.nmat * (4 * kMatF);
@@ -1634,7 +1464,7 @@ hipError_t launch_t(const DevScene& sc, const FrameParams& fp, int block, float*
     int dev = 0, cus = 0, per_cu = 0;
     hipError_t e = hipGetDevice(&dev);
     if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    const void* kfn = RESUME ? (const void*)render_resume_kernel<COUNT, LOG, SMEM, OVF, STEP, COMPACT>
+    const void* kfn = RESUME ? (const void*)render_resume_kernel<COUNT, LOG, SMEM, OVF, STEP>
                              : (const void*)render_kernel<TRAV, COUNT, LOG, SMEM, OVF, BRUTE ? 1 : 0>;
     if (e == hipSuccess) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kfn, block, lds);
     if (e != hipSuccess) return e;
@@ -1665,13 +1495,15 @@ hipError_t launch_t(const DevScene& sc, const FrameParams& fp, int block, float*
         if (e != hipSuccess) return e;
         grid = std::min(need, (int64_t)std::max(1, cus) * std::max(1, std::min(per_cu_t, cap_cu)));
     }
-    e = hipMemsetAsync(d_work, 0, sizeof(unsigned int), stream);
+    e = hipMemsetAsync(d_work, 0, (size_t)kGroups * kCounterStride, stream);
     if (e != hipSuccess) return e;
-    // the per-launch constants live after the counter in the same scratch block
-    LaunchConst* lc = reinterpret_cast<LaunchConst*>(reinterpret_cast<char*>(d_work) + 64);
+    // the per-launch constants live after the counters in the same scratch block
+    static_assert(kConstOffset >= kGroups * kCounterStride && kConstOffset + sizeof(LaunchConst) <= kWorkBytes,
+                  "work block layout");
+    LaunchConst* lc = reinterpret_cast<LaunchConst*>(reinterpret_cast<char*>(d_work) + kConstOffset);
     hipLaunchKernelGGL(make_const_kernel, dim3(1), dim3(64), 0, stream, f, lc);
     if (RESUME)
-        hipLaunchKernelGGL((render_resume_kernel<COUNT, LOG, SMEM, OVF, STEP, COMPACT>), dim3((unsigned)grid), dim3(block), lds, stream,
+        hipLaunchKernelGGL((render_resume_kernel<COUNT, LOG, SMEM, OVF, STEP>), dim3((unsigned)grid), dim3(block), lds, stream,
                            sc, f, d_out, d_counts, d_work, (const LaunchConst*)lc);
     else if (BRUTE && f.team > 1)
         hipLaunchKernelGGL((render_kernel<TRAV, COUNT, LOG, SMEM, OVF, BRUTE ? 2 : 0>), dim3((unsigned)grid),
@@ -1750,8 +1582,7 @@ hipError_t launch_debug_trace(const DevScene& sc, int traversal, const float* ra
     s2.stack_ovf = nullptr;
     const int depth = traversal == TRAV_REF ? REF_STACK : 2 * s2.stack_lds;
     size_t lds = (size_t)depth * block * sizeof(int);
-    if (traversal != TRAV_REF && sc.nbrute > 0 && RT_BRUTE_COMPACT)
-        lds = std::max(lds, (size_t)(block / 64) * BRUTE_WAVE_LDS);
+    if (traversal != TRAV_REF && sc.nbrute > 0) lds = std::max(lds, (size_t)(block / 64) * BRUTE_WAVE_LDS);
     if (traversal == TRAV_REF)
         hipLaunchKernelGGL(debug_trace_kernel<TRAV_REF>, dim3((unsigned)((n + block - 1) / block)), dim3(block), lds,
                            stream, s2, rays, out, n);
@@ -1764,14 +1595,6 @@ hipError_t launch_debug_trace(const DevScene& sc, int traversal, const float* ra
 template <bool COUNT, bool STEP>
 hipError_t launch_resume(const DevScene& sc, const FrameParams& fp, int block, float* d_out,
                          unsigned long long* d_counts, unsigned int* d_work, hipStream_t stream, bool smem, bool ovf) {
-    // item steps on the compact 48-byte nodes: three loads per item instead of four
-    if (STEP && !smem && fp.compact && sc.nodes48 && sc.tri2) {
-        if (ovf)
-            return launch_t<TRAV_FAST, COUNT, false, false, true, true, false, true, true>(sc, fp, block, d_out,
-                                                                                         d_counts, d_work, stream);
-        return launch_t<TRAV_FAST, COUNT, false, false, true, false, false, true, true>(sc, fp, block, d_out, d_counts,
-                                                                                      d_work, stream);
-    }
     if (smem)
         return launch_t<TRAV_FAST, COUNT, false, true, true, false, false, STEP>(sc, fp, block, d_out, d_counts,
                                                                                  d_work, stream);
@@ -1786,19 +1609,19 @@ template <bool COUNT>
 hipError_t launch_fast(const DevScene& sc, const FrameParams& fp, int block, float* d_out,
                        unsigned long long* d_counts, unsigned int* d_work, hipStream_t stream) {
     const size_t scene_bytes = (size_t)(kNodeF4 * sc.nnodes + 3 * sc.ntri) * sizeof(float4);
-    const bool smem = sc.ntri > 0 && sc.nbrute == 0 && scene_bytes <= (size_t)RT_LDS_SCENE_MAX;
+    const bool smem = sc.ntri > 0 && sc.nbrute == 0 && scene_bytes <= kLdsSceneMax;
     const bool ovf = sc.nbrute == 0 && sc.stack_lds < sc.depth;
     const bool resume = sc.ntri > 0 && sc.nbrute == 0 && fp.resume_min > 0;
     if (resume) {
         const bool step = fp.step == 1 ||
-                          (fp.step == 0 && (size_t)sc.nnodes * kNodeF4 * 16 <= (size_t)RT_STEP_MAX_BYTES);
+                          (fp.step == 0 && (size_t)sc.nnodes * kNodeF4 * 16 <= kStepMaxBytes);
         return step ? launch_resume<COUNT, true>(sc, fp, block, d_out, d_counts, d_work, stream, smem, ovf)
                     : launch_resume<COUNT, false>(sc, fp, block, d_out, d_counts, d_work, stream, smem, ovf);
     }
     // BRUTE stages the scene in LDS: only while two blocks still fit a CU
     const size_t brute_lds = (size_t)(block / 64) * BRUTE_WAVE_LDS + (size_t)sc.nbrute * 48 +
                              (size_t)sc.nbox * 32 + (size_t)sc.ntri * 64 + (size_t)sc.nmat * (4 * kMatF);
-    if (sc.ntri > 0 && sc.nbrute > 0 && RT_BRUTE_COMPACT && RT_BRUTE_LDS && brute_lds <= 80 * 1024)
+    if (sc.ntri > 0 && sc.nbrute > 0 && brute_lds <= 80 * 1024)
         return launch_t<TRAV_FAST, COUNT, false, false, false, false, true>(sc, fp, block, d_out, d_counts, d_work,
                                                                             stream);
     if (smem) return launch_t<TRAV_FAST, COUNT, false, true>(sc, fp, block, d_out, d_counts, d_work, stream);

@@ -322,20 +322,16 @@ def test_traversal_step_modes_render_identically(kl, case):
     sc, cam, env, npix, spp, mb, ibl = W.PARITY_CASES[case].inputs()
     frames = []
     try:
-        for mode, compact in ((1, 1), (1, 0), (2, 1), (0, 1)):
+        for mode in (1, 2, 0):
             kl.native.set_option("step", mode)
-            kl.native.set_option("compact", compact)   # item steps on the 48-byte nodes (refs in box bits)
             frames.append(_launch(kl, sc, cam, env, npix, spp, mb, ibl, "fast"))
     finally:
         kl.native.set_option("step", 0)
-        kl.native.set_option("compact", 1)
     for f in frames[1:]:
         np.testing.assert_array_equal(frames[0], f)
     np.testing.assert_array_equal(frames[0], _oracle(sc, cam, env, npix, spp, mb, ibl))
     with pytest.raises(_native.NativeError, match="step"):
         kl.native.set_option("step", 3)
-    with pytest.raises(_native.NativeError, match="compact"):
-        kl.native.set_option("compact", 2)
 
 
 @pytest.mark.parametrize("case", ["cornell_64_s4", "monkey_c3_64_s4"])
