@@ -11,17 +11,24 @@ over RCCL and assembles the frame.  K steps are timed between barrier +
 synchronize fences; the max over ranks is reported.  value = W*H*spp / time in
 Msamples/s (whole job; the frame size is fixed, so scaling is "strong").
 
-Extra fields:
-  roofline     -- dominant kernel (render_kernel): algorithmic bytes per launch
-                  (this build's own traversal counters x bytes per unit, see
-                  DESIGN.md) / average kernel time from HIP events on the launch
-                  stream; peak = 8 TB/s HBM; traffic = PMC-measured HBM bytes per
-                  launch from profiles/ (rocprofv3) when present, else null;
-                  traffic_frac = that measured traffic / kernel time / peak.  On a
-                  cache-resident scene (C2) frac > 1: the algorithmic bytes are
-                  served from LDS / scalar cache / L2, not HBM.
-  cpu_baseline -- the CPU oracle (a C restatement of the reference kernel, OpenMP)
-                  timed on this host on a bounded row sample of the same frame.
+Extra fields (DESIGN.md 5 derives every number):
+  roofline      -- the render kernel against the bound of the path that ran:
+                   * brute-force path (scenes of <= brute_max triangles: C1/C2):
+                     bound "valu", achieved = algorithmic VALU lane-operations per
+                     launch (VALU_OPS per unit x the unit counts of the SAME
+                     traversal, rt_count_work_detail) / the kernel's average
+                     duration from HIP events on its stream; peak = the FP32 vector
+                     issue rate (256 CUs x 4 SIMD x 32 lanes x 2.4 GHz).
+                   * tree walk (C3-C5): bound "hbm", achieved = SURVEY 8(d)
+                     algorithmic bytes per launch / kernel time, peak 8 TB/s.
+                   traffic = PMC-measured HBM bytes per launch (committed rocprofv3
+                   summary in profiles/), issued = PMC-measured VALU lane slots
+                   (SQ_INSTS_VALU x 64) per launch, when committed.
+  host_boundary -- rt_render (launch_Raytracing's blocking C-ABI: kernel + copy of
+                   the frame into caller memory), timed over the same W/K steps.
+  configs       -- N=1 only: C3 and C4 timed the same way (2 steps, 1 warmup).
+  cpu_baseline  -- the CPU oracle (a C restatement of the reference kernel, OpenMP)
+                   timed on this host on a bounded row sample of the same frame.
 """
 from __future__ import annotations
 
@@ -38,7 +45,25 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 METRIC = "Msamples/s Cornell box 1024x1024 64spp; 1/2/4/8-GPU scaling; HBM %peak"
-HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
+VALU_PEAK_TOPS = 78.6432       # 256 CUs x 4 SIMD x 32 lanes/clk x 2.4 GHz: VALU lane-ops/s (157.3 TFLOPS FP32 = 2 x this, FMA)
+
+# Algorithmic VALU lane-operations per unit of work ("VALU roofline"): IEEE basic
+# operations (+ - * / sqrt fma min max compare) and integer ops of the numerics contract
+# (csrc/rtm.h: Cephes sincos 27, acos/asin 15, atan2 26, normalize 8, quaternion product 19), counted
+# on the reference's per-ray arithmetic (Raytracing.cl / MathLib.cl).
+VALU_OPS = {
+    "box_tests": 25,      # slab test: 6 sub + 6 mul + 10 min/max + entry compare (MathLib.cl:167-199)
+    "tri_tests": 56,      # Moller-Trumbore: 2 cross, 4 dot, 1 div, 3 scale, 8 compares (MathLib.cl:117-160)
+    "rays": 8,            # 1/d (3 div) + hit bookkeeping
+    "ev_diffuse": 141,    # 2 rand, sqrt, sincos, rotateVec + normalize, invPdf, Lambert, origin, attenuation
+    "ev_glossy": 239,     # 2 rand, acos, 2 sincos, rotateVec, BRDF_GGX (75), origin, attenuation
+    "ev_glass": 28,       # invPdf, origin, attenuation
+    "sun_terms": 11,      # Raytracing.cl:115-137 without the IBL lookup
+    "env_lookups": 164,   # 2 rotateVec, atan2, asin, texel address + 2x2 mean (MathLib.cl:72-90)
+    "samples": 5,         # accumulate + loop
+    "pixels": 148,        # genCameraRay (3 rotateVec, normalize), seeds, mean + clamp (Raytracing.cl:18-37, 211-220)
+}
 
 
 def _dist_env():
@@ -48,17 +73,62 @@ def _dist_env():
     return rank, world, local
 
 
-def _pmc_traffic(config_name: str):
-    """Per-launch HBM bytes from the newest committed rocprofv3 PMC summary for this workload."""
+def _profile(config_name: str):
+    """The newest committed rocprofv3 PMC summary for this workload (profiles/*pmc*<workload>*.json)."""
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"*pmc*{config_name}*.json")))
     if not files:
-        return None
+        return {}
     try:
         with open(files[-1]) as f:
             d = json.load(f)
-        return d.get("hbm_bytes_per_launch")
+        d["_file"] = os.path.relpath(files[-1], ROOT)
+        return d
     except (OSError, ValueError):
-        return None
+        return {}
+
+
+def valu_ops(cnt: dict, pixels: int) -> float:
+    return float(sum(VALU_OPS[k] * (pixels if k == "pixels" else cnt[k]) for k in VALU_OPS))
+
+
+def alg_bytes(cnt: dict, wb: dict, pixels: int) -> float:
+    # SURVEY 8(d): 32 B per box tested (a FAST node = 64 B: both children), 36 B per triangle test,
+    # 40 B per ray hit record, 16 B per IBL lookup, + the tile written (12 B per pixel)
+    return (cnt["node_fetches"] * wb["node_fetch"] + cnt["tri_tests"] * wb["tri_test"] + cnt["rays"] * wb["ray"]
+            + cnt["env_lookups"] * wb["env_lookup"] + pixels * 12.0)
+
+
+def roofline(ctx, cnt: dict, kernel_ms: float, pixels: int, workload: str) -> dict:
+    info = ctx.scene_info()
+    brute = info["brute_records"] > 0
+    prof = _profile(workload)
+    sec = kernel_ms * 1e-3
+    ops = valu_ops(cnt, pixels)
+    byt = alg_bytes(cnt, ctx.work_bytes(), pixels)
+    traffic = prof.get("hbm_bytes_per_launch")
+    issued = prof.get("valu_lane_slots_per_launch")
+    valu = {"achieved": round(ops / sec / 1e12, 3), "peak": VALU_PEAK_TOPS, "unit": "Tops/s",
+            "frac": round(ops / sec / 1e12 / VALU_PEAK_TOPS, 4), "alg_ops_per_launch": int(ops),
+            "issued": issued, "issued_frac": (round(issued / sec / 1e12 / VALU_PEAK_TOPS, 4) if issued else None)}
+    hbm = {"achieved": round(byt / sec / 1e9, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+           "frac": round(byt / sec / 1e9 / HBM_PEAK_GBS, 4), "alg_bytes_per_launch": int(byt),
+           "traffic": traffic, "traffic_frac": (round(traffic / sec / 1e9 / HBM_PEAK_GBS, 5) if traffic else None)}
+    main, other, bound = (valu, hbm, "valu") if brute else (hbm, valu, "hbm")
+    out = {"bound": bound}
+    out.update(main)
+    if bound == "valu":   # the measured HBM traffic of the same kernel beside the VALU bound
+        out["traffic"], out["traffic_frac"] = hbm["traffic"], hbm["traffic_frac"]
+    out["kernel_ms"] = round(kernel_ms, 4)
+    out["path"] = (f"brute force ({info['brute_boxes']} distinct leaf boxes, {info['brute_records']} triangles)"
+                   if brute else f"SAH tree walk ({info['nodes']} nodes, {info['tris']} triangles)")
+    out["other_bound"] = {"bound": "hbm" if brute else "valu", **other}
+    out["counts_per_sample"] = {k: round(cnt[k] / max(1, cnt["samples"]), 4)
+                                for k in ("box_tests", "tri_tests", "rays", "ev_diffuse", "ev_glossy", "ev_glass",
+                                          "sun_terms", "env_lookups", "node_fetches")}
+    out["model"] = "VALU_OPS / SURVEY 8(d) bytes per unit in bench.py x counts of the same launch (DESIGN.md 5)"
+    if prof:
+        out["profile"] = prof.get("_file")
+    return out
 
 
 def cpu_baseline(wl, scene, ibl, cam, env, target_s: float = 10.0):
@@ -81,7 +151,41 @@ def cpu_baseline(wl, scene, ibl, cam, env, target_s: float = 10.0):
     samples = rows * W * wl.spp
     return {"value": samples / dt / 1e6, "unit": "Msamples/s", "cores": threads, "kind": "port",
             "sample": f"rows 0::{step} of the {W}x{H} frame ({rows} rows) at {wl.spp} spp = {samples} samples "
-                      f"in {dt:.2f} s; oracle/rt_oracle.c (C restatement of the reference kernel), OpenMP"}
+                      f"in {dt:.2f} s; oracle/rt_oracle.c (C restatement of the reference kernel), OpenMP",
+            "calibration": "C2 in the build container, 8 threads: oracle 1.90 Msamples/s vs the reference kernel "
+                           "itself 2.06-2.14 (BASELINE.md 2): 0.89-0.92x (DESIGN.md 5)"}
+
+
+def time_config(ctx_factory, name: str, steps: int, warmup: int):
+    """One-GPU device-resident timing of another BASELINE config (C3/C4), same method as the headline."""
+    import torch
+    from ensem3a_openclraytracer_amd import workloads as Wk
+    wl = Wk.CONFIGS[name]
+    scene, cam, env, npix, spp, mb, ibl = wl.inputs()
+    ctx = ctx_factory()
+    ctx.set_scene(scene.V_p, scene.V_n, scene.V_uv, scene.faceData, scene.materialData, scene.BVH.exportArray)
+    ctx.set_env(ibl)
+    out = torch.empty(3 * npix, dtype=torch.float32, device="cuda")
+    stream = torch.cuda.current_stream()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+    for _ in range(warmup):
+        ctx.render_device(cam, env, npix, spp, mb, 0, 1, out.data_ptr(), stream.cuda_stream)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(steps):
+        ev[i][0].record(stream)
+        ctx.render_device(cam, env, npix, spp, mb, 0, 1, out.data_ptr(), stream.cuda_stream)
+        ev[i][1].record(stream)
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / steps
+    kernel_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    cnt = ctx.count_work_detail(cam, env, npix, spp, mb)
+    rf = roofline(ctx, cnt, kernel_ms, npix, wl.name)
+    ctx.close()
+    return {"workload": wl.name, "value": round(npix * spp / dt / 1e6, 3), "unit": "Msamples/s",
+            "ms_per_step": round(dt * 1e3, 3), "steps": steps, "warmup": warmup,
+            "roofline": {k: rf[k] for k in ("bound", "achieved", "peak", "unit", "frac", "kernel_ms", "path")},
+            "valu_frac": rf["frac"] if rf["bound"] == "valu" else rf["other_bound"]["frac"]}
 
 
 def main():
@@ -94,6 +198,7 @@ def main():
     ap.add_argument("--bvh", default="sah", choices=["sah", "reference"])
     ap.add_argument("--block", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-extra", action="store_true", help="skip the C3/C4 lines and the host-boundary timing")
     ap.add_argument("--check", action="store_true",
                     help="N>1: rank 0 re-renders the whole frame alone and compares it with the gathered one")
     args = ap.parse_args()
@@ -121,13 +226,17 @@ def main():
             dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", local))
     coll = "cpu" if rehearsal else "cuda"   # where collective buffers live
 
+    def make_ctx():
+        c = _native.Context(device_ids=[local])
+        c.set_option("traversal", _native.RT_TRAVERSAL_FAST if args.traversal == "fast" else _native.RT_TRAVERSAL_REF)
+        c.set_option("bvh", _native.RT_BVH_SAH if args.bvh == "sah" else _native.RT_BVH_REFERENCE)
+        if args.block:
+            c.set_option("block", args.block)
+        return c
+
     wl = Wk.CONFIGS[args.config]
     scene, cam, env, npix, spp, mb, ibl = wl.inputs()
-    ctx = _native.Context(device_ids=[local])
-    ctx.set_option("traversal", _native.RT_TRAVERSAL_FAST if args.traversal == "fast" else _native.RT_TRAVERSAL_REF)
-    ctx.set_option("bvh", _native.RT_BVH_SAH if args.bvh == "sah" else _native.RT_BVH_REFERENCE)
-    if args.block:
-        ctx.set_option("block", args.block)
+    ctx = make_ctx()
     ctx.set_scene(scene.V_p, scene.V_n, scene.V_uv, scene.faceData, scene.materialData, scene.BVH.exportArray)
     ctx.set_env(ibl)
     width = int(cam[6])
@@ -170,21 +279,10 @@ def main():
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed, kernel_ms = float(tt[0]), float(tt[1])
 
-    # algorithmic bytes of one launch on this rank: counters of the same traversal x bytes per unit
-    # The bytes are those of the tree walk (FAST over the SAH BVH2): scenes of <= 64 triangles run the
-    # lock-step brute-force path instead, which reads every triangle record per ray from the scalar
-    # cache -- more bytes by construction, so it is not what the roofline is priced on.
-    ctx.set_option("brute_max", 0)
-    cnt = ctx.count_work(cam, env, npix, spp, mb, rank, world)
-    ctx.set_option("brute_max", 64)
-    wb = ctx.work_bytes()
-    alg_bytes = (cnt["node_fetches"] * wb["node_fetch"] + cnt["tri_tests"] * wb["tri_test"]
-                 + cnt["rays"] * wb["ray"] + cnt["env_lookups"] * wb["env_lookup"]
-                 + D.tile_rows(npix, width, rank, world) * width * 12)   # + the tile written
-    if world > 1:
-        tb = torch.tensor([alg_bytes], dtype=torch.float64, device=coll)
-        dist.all_reduce(tb, op=dist.ReduceOp.MAX)
-        alg_bytes = float(tb[0])
+    # work counters of the same traversal on this rank's tile (instrumented launch, not timed)
+    cnt = ctx.count_work_detail(cam, env, npix, spp, mb, rank, world)
+    tile_pixels = D.tile_rows(npix, width, rank, world) * width
+    rf = roofline(ctx, cnt, kernel_ms, tile_pixels, wl.name)
 
     frame_check = None
     if args.check and world > 1:
@@ -201,8 +299,6 @@ def main():
         samples = npix * spp
         ms_per_step = elapsed / args.steps * 1e3
         value = samples * args.steps / elapsed / 1e6
-        achieved = alg_bytes / (kernel_ms * 1e-3) / 1e9
-        traffic = _pmc_traffic(wl.name)   # measured HBM bytes per launch (committed rocprofv3 PMC summary)
         line = {
             "metric": METRIC, "value": round(value, 3), "unit": "Msamples/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4),
@@ -212,36 +308,36 @@ def main():
                        "spp": spp, "max_bounce": mb, "traversal": args.traversal, "bvh": args.bvh,
                        "parallelism": f"row-interleaved x{world}" + (
                            (" + gloo gather (one-GPU rehearsal)" if rehearsal else " + RCCL gather") if world > 1 else "")},
-            "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                         "traffic_frac": (round(traffic / (kernel_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 5)
-                                          if traffic else None),
-                         "kernel_ms": round(kernel_ms, 4), "alg_bytes_per_launch": int(alg_bytes),
-                         "bytes_model": "SURVEY 8(d): 32 B/box tested (FAST node = 2 boxes), 36 B/triangle test, "
-                                        "40 B/ray hit record, 16 B/IBL lookup; counts of this build's SAH tree walk",
-                         "counts_per_sample": {k: round(v / (samples / world), 4) for k, v in cnt.items()}},
+            "roofline": rf,
         }
         if frame_check is not None:
             line["frame_check"] = f"gathered {world}-rank frame vs one-device render: {frame_check}"
-        if world == 1:
-            # the drop-in boundary's own rate: blocking rt_render into host memory (kernel + PCIe read-back)
+        if world == 1 and not args.no_extra:
+            # the drop-in boundary's own rate: blocking rt_render into host memory (kernel + read-back),
+            # same warmup / steps as the headline
             host = np.zeros(3 * npix, np.float32)
-            ctx.render(cam, env, npix, spp, mb, out=host)
-            t0 = time.perf_counter()
-            for _ in range(3):
+            for _ in range(args.warmup):
                 ctx.render(cam, env, npix, spp, mb, out=host)
-            dt = (time.perf_counter() - t0) / 3
+            t0 = time.perf_counter()
+            for _ in range(args.steps):
+                ctx.render(cam, env, npix, spp, mb, out=host)
+            dt = (time.perf_counter() - t0) / args.steps
             line["host_boundary"] = {"value": round(samples / dt / 1e6, 3), "unit": "Msamples/s",
-                                     "ms_per_frame": round(dt * 1e3, 3),
-                                     "what": "rt_render (launch_Raytracing's C-ABI): kernel + device-to-host copy "
-                                             "of the frame into caller memory, scene already uploaded"}
+                                     "ms_per_frame": round(dt * 1e3, 3), "steps": args.steps,
+                                     "what": "rt_render (launch_Raytracing's C-ABI): kernel + copy of the frame "
+                                             "into caller memory, scene already uploaded"}
+        if world == 1 and not args.no_extra and args.config == "C2":
+            ctx.close()
+            ctx = None
+            line["configs"] = {c: time_config(make_ctx, c, 2, 1) for c in ("C3", "C4")}
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(wl, scene, ibl, cam, env)
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
-    ctx.close()
+    if ctx is not None:
+        ctx.close()
 
 
 if __name__ == "__main__":

@@ -24,7 +24,7 @@ RT_BVH_SAH = 1
 # Every symbol of include/rt_api.h and include/rt_debug.h (checked by tests).
 EXPORTED = (
     "rt_create", "rt_destroy", "rt_last_error", "rt_set_scene", "rt_set_env", "rt_set_option",
-    "rt_render", "rt_render_device", "rt_tile_rows", "rt_count_work", "rt_work_bytes", "rt_gamma",
+    "rt_render", "rt_render_device", "rt_tile_rows", "rt_count_work", "rt_count_work_detail", "rt_work_bytes", "rt_gamma",
     "rt_render_rgb8", "rt_rgb8_device", "rt_rgb8",
     "rt_bvh_build", "rt_device_count", "rt_debug_math", "rt_debug_trace", "rt_debug_scene_info", "rt_debug_pixel_log",
     "rt_debug_wave_counts",
@@ -44,6 +44,19 @@ class NativeError(RuntimeError):
         self.status = status
 
 
+def _preload_hip_runtime() -> None:
+    import importlib.util
+    try:
+        spec = importlib.util.find_spec("torch")
+    except (ImportError, ValueError):
+        spec = None
+    for d in (spec.submodule_search_locations or []) if spec else []:
+        p = os.path.join(d, "lib", "libamdhip64.so")
+        if os.path.exists(p):
+            ctypes.CDLL(p, mode=ctypes.RTLD_GLOBAL)
+            return
+
+
 def lib():
     """Load (once) and return the native library; raise loudly when absent."""
     global _lib
@@ -52,13 +65,13 @@ def lib():
     with _lock:
         if _lib is not None:
             return _lib
-        # torch ships its own libamdhip64.so.7 with the same SONAME as ROCm's: whichever is loaded
-        # first serves the whole process.  Load torch's first (when torch is installed) so torch
-        # tensors/streams and this library share ONE HIP runtime.
-        try:
-            import torch  # noqa: F401
-        except ImportError:
-            pass
+        # torch ships its own HIP runtime (torch/lib/libamdhip64.so, SONAME libamdhip64.so.7, the
+        # same SONAME as ROCm's): whichever is loaded first serves the whole process, and torch
+        # cannot initialise its GPUs on ROCm's.  So when torch is installed its runtime is loaded
+        # first -- as a plain shared library, without importing torch: the single-GPU drop-in path
+        # (KernelLauncher) needs no torch, and a torch imported later finds its own runtime
+        # already loaded (tests/test_gpu_boundary.py).
+        _preload_hip_runtime()
         lib_path = os.environ.get("ENSEM3A_RT_LIB", LIB)  # experimental variants (tools/variants.py)
         if not os.path.exists(lib_path):
             raise RuntimeError(
@@ -76,6 +89,7 @@ def lib():
             "rt_render_device": (_i32, [_c_p, _i32, _c_p, _c_p, _i64, _i32, _i32, _i32, _i32, _c_p, _c_p]),
             "rt_tile_rows": (_i64, [_i64, _i32, _i32, _i32]),
             "rt_count_work": (_i32, [_c_p, _c_p, _c_p, _i64, _i32, _i32, _i32, _i32, _c_p]),
+            "rt_count_work_detail": (_i32, [_c_p, _c_p, _c_p, _i64, _i32, _i32, _i32, _i32, _c_p]),
             "rt_work_bytes": (_i32, [_c_p, _c_p]),
             "rt_gamma": (_i32, [_c_p, _c_p, _c_p, _i64]),
             "rt_render_rgb8": (_i32, [_c_p, _c_p, _c_p, _i64, _i32, _i32, _i32, _c_p]),
@@ -198,6 +212,18 @@ class Context:
                                         int(row0), int(row_step), out.ctypes.data))
         return dict(zip(("node_fetches", "tri_tests", "rays", "env_lookups", "stack_drops"), map(int, out)))
 
+    COUNT_KEYS = ("node_fetches", "tri_tests", "rays", "env_lookups", "stack_drops", "wave_trav_iters",
+                  "wave_render_iters", "cycles_shade", "cycles_trav", "box_tests", "ev_diffuse", "ev_glossy",
+                  "ev_glass", "sun_terms", "samples")
+
+    def count_work_detail(self, cam, env, npix, spp, max_bounce, row0=0, row_step=1):
+        """rt_count_work_detail: every work counter of the instrumented render of the tile."""
+        c, e = f32(cam), f32(env)
+        out = np.zeros(16, dtype=np.uint64)
+        self._check(lib().rt_count_work_detail(self.handle, ptr(c), ptr(e), int(npix), int(spp), int(max_bounce),
+                                               int(row0), int(row_step), out.ctypes.data))
+        return {k: int(v) for k, v in zip(self.COUNT_KEYS, out)}
+
     def work_bytes(self):
         out = np.zeros(4, dtype=np.float64)
         self._check(lib().rt_work_bytes(self.handle, out.ctypes.data))
@@ -271,9 +297,10 @@ class Context:
         return {k: int(v) for k, v in zip(keys, out)}
 
     def scene_info(self):
-        out = np.zeros(4, dtype=np.int64)
+        out = np.zeros(8, dtype=np.int64)
         self._check(lib().rt_debug_scene_info(self.handle, out.ctypes.data))
-        return dict(fast_ok=bool(out[0]), depth=int(out[1]), nodes=int(out[2]), tris=int(out[3]))
+        return dict(fast_ok=bool(out[0]), depth=int(out[1]), nodes=int(out[2]), tris=int(out[3]),
+                    brute_records=int(out[4]), brute_boxes=int(out[5]))
 
 
 def parse_obj(text):

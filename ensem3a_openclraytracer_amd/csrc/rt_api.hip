@@ -927,6 +927,11 @@ int rt_count_work(rt_ctx* ctx, const float cam[10], const float env[5], int64_t 
     return count_all(ctx, cam, env, npix, spp, max_bounce, row0, row_step, counts, 5);
 }
 
+int rt_count_work_detail(rt_ctx* ctx, const float cam[10], const float env[5], int64_t npix, int spp, int max_bounce,
+                         int row0, int row_step, uint64_t counts[16]) {
+    return count_all(ctx, cam, env, npix, spp, max_bounce, row0, row_step, counts, 16);
+}
+
 int rt_debug_wave_counts(rt_ctx* ctx, const float cam[10], const float env[5], int64_t npix, int spp, int max_bounce,
                          uint64_t counts[9]) {
     return count_all(ctx, cam, env, npix, spp, max_bounce, 0, 1, counts, 9);
@@ -1035,12 +1040,16 @@ int rt_debug_pixel_log(rt_ctx* ctx, int traversal, const float cam[10], const fl
     return RT_OK;
 }
 
-int rt_debug_scene_info(rt_ctx* ctx, int64_t out[4]) {
+int rt_debug_scene_info(rt_ctx* ctx, int64_t out[8]) {
     if (!ctx || !out) return set_err(ctx, RT_ERR_ARG, "bad arguments");
     out[0] = ctx->hs.fast_ok ? 1 : 0;
     out[1] = ctx->hs.depth;
     out[2] = ctx->hs.nnodes;
     out[3] = ctx->hs.ntri;
+    out[4] = effective_traversal(ctx) == RT_TRAVERSAL_FAST ? ctx->hs.nbrute : 0;
+    out[5] = out[4] ? ctx->hs.nbox : 0;
+    out[6] = 0;
+    out[7] = 0;
     return RT_OK;
 }
 

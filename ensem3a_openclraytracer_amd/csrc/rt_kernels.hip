@@ -46,14 +46,26 @@ struct Hit {
     int tri;  // < 0: miss
 };
 
+// Work counters of the instrumented (COUNT) kernels, summed over the launch; the order is the
+// public one of rt_count_work_detail (include/rt_api.h).
 struct Cnt {
     unsigned long long nodes, tris, rays, env, dropped;
     unsigned long long wave_trav;   // traversal-loop iterations issued per wave (any lane active)
     unsigned long long wave_outer;  // render-loop iterations per wave
     unsigned long long cyc_shade;   // resumable kernel, per wave: clock cycles outside the traversal rounds
     unsigned long long cyc_trav;    //   ... and inside them
+    unsigned long long boxes;       // ray-box slab tests (a FAST node tests 2, a REF node 1, brute force: distinct leaf boxes)
+    unsigned long long diffuse, glossy, glass;   // shading events (naiveGI bounces) by material type 1 / 2 / 3
+    unsigned long long sun;         // sun terms evaluated (Raytracing.cl:115-137)
+    unsigned long long samples;     // samples completed
 };
-constexpr int NCOUNTS = 9;
+constexpr int NCOUNTS = 15;
+
+__device__ __forceinline__ void count_event(Cnt& c, int type) {
+    if (type == 1) c.diffuse++;
+    else if (type == 2) c.glossy++;
+    else c.glass++;
+}
 
 // COUNT builds: the lowest active lane of the wave counts one wave-level iteration.
 __device__ __forceinline__ void count_wave(unsigned long long& x) {
@@ -100,7 +112,7 @@ __device__ Hit trace_ref(const DevScene& S, rtm_f3 o, rtm_f3 d, int* __restrict_
         if (COUNT) count_wave(c.wave_trav);
         const int curr = stk[top * B];
         --top;
-        if (COUNT) c.nodes++;
+        if (COUNT) { c.nodes++; c.boxes++; }
         const float* nd = S.bvh9 + 9 * curr;
         const float tx1 = (nd[2] - o.x) / d.x, tx2 = (nd[5] - o.x) / d.x;
         float tmin = fminf(tx1, tx2), tmax = fmaxf(tx1, tx2);
@@ -287,7 +299,7 @@ __device__ Hit trace_fast(const DevScene& S, const float4* __restrict__ nodes, c
     while (true) {
         if (COUNT) count_wave(c.wave_trav);
         if (item >= 0) {
-            if (COUNT) c.nodes++;
+            if (COUNT) { c.nodes++; c.boxes += 2; }
             const char* np = nb + (SOA ? 16u : 16u * kNodeF4) * (unsigned)item;
             const int next = node_step<OVF>(np, kstride, o, ix, iy, iz, best.k * CULL_MARGIN, st, soff);
             if (next != INT_MIN) {
@@ -464,6 +476,7 @@ __device__ Hit trace_brute_compact(const DevScene& S, rtm_f3 o, rtm_f3 d, char* 
                 if (g0 + j >= S.nbox) break;   // padding (never hit; skipped so the counters stay exact)
                 const int qa = __float_as_int(bx[2 * j + 1].z), qb = __float_as_int(bx[2 * j + 1].w);
                 if (COUNT) {   // counted per record (one leaf box test each, as in the tree walk)
+                    c.boxes++;
                     count_wave(c.wave_trav); c.nodes++;
                     if (qb >= 0) { count_wave(c.wave_trav); c.nodes++; }
                 }
@@ -486,7 +499,7 @@ __device__ Hit trace_brute_compact(const DevScene& S, rtm_f3 o, rtm_f3 d, char* 
                 pass = box_hit(tn, tx, bk * CULL_MARGIN);
                 qa = __float_as_int(b1.z);
                 qb = __float_as_int(b1.w);
-                if (COUNT) c.nodes += qb >= 0 ? 2 : 1;
+                if (COUNT) { c.nodes += qb >= 0 ? 2 : 1; c.boxes++; }
             }
             enqueue(pass, (unsigned)qa, -1);
             enqueue(pass && qb >= 0, (unsigned)qb, -1);
@@ -807,7 +820,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) r
     const int B = blockDim.x;
     int* stk = lds_stack + threadIdx.x;
     const LaneStack lst = lane_stack(S, lds_stack);
-    Cnt c{0, 0, 0, 0, 0, 0, 0, 0, 0};
+    Cnt c{};
     // BRUTE (small scenes, brute-force traversal): the MT batches' triangle records and all shading
     // tables (hit records, hemisphere frames, materials) are staged in LDS behind the per-wave regions
     const float4* mtrec = nullptr;
@@ -928,6 +941,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) r
                     const rtm_f3 nn = xyz(f2);
                     float invPdf = 0.0f;
                     rtm_f3 brdf = rtm_v3(0, 0, 0);
+                    if (COUNT) count_event(c, cm.type);
                     if (cm.type == 1) {
                         Bd = hemi_cosine(n, tframe[3 * tri], tframe[3 * tri + 1], f2, &seed1, &seed0,
                                          &invPdf);
@@ -953,6 +967,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) r
             if (done) {
                 if (LOG && logme) log_event(F, 3.0f, s + 1, rtm_v3(0, 0, 0), rtm_v3(0, 0, 0), 0.0f, 0, so);
                 acc = rtm_add(acc, so);
+                if (COUNT) c.samples++;
                 ++s;
                 if (s >= spp) {
                     phase = FETCH;
@@ -1015,6 +1030,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) r
         }
         if (sun_hit != -2) {  // SUN (Raytracing.cl:115-137)
             rtm_f3 sunLight = rtm_v3(0, 0, 0);
+            if (COUNT) c.sun++;
             const Mat cm = load_mat(tmat, __float_as_int(tshade[tri].w));
             if (sun_hit < 0 && cm.type != 3) sunLight = rtm_v3(e3, e3, e3);
             if (sun_hit >= 0) {
@@ -1028,6 +1044,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) r
         if (finish) {
             if (LOG && logme) log_event(F, 3.0f, s + 1, rtm_v3(0, 0, 0), rtm_v3(0, 0, 0), 0.0f, 0, so);
             acc = rtm_add(acc, so);
+            if (COUNT) c.samples++;
             ++s;
             if (s >= spp) {
                 if (team_leader) store_pixel(out, p, acc, spp);
@@ -1040,9 +1057,12 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) r
         }
     }
     if (COUNT) {
-        if (!team_leader) c.env = 0;   // a team's lanes repeat its pixel's shading: counted once
+        if (!team_leader) {   // a team's lanes repeat its pixel's shading: counted once
+            c.env = 0; c.diffuse = 0; c.glossy = 0; c.glass = 0; c.sun = 0; c.samples = 0;
+        }
         unsigned long long v[NCOUNTS] = {c.nodes, c.tris, c.rays, c.env, c.dropped, c.wave_trav, c.wave_outer,
-                                          c.cyc_shade, c.cyc_trav};
+                                          c.cyc_shade, c.cyc_trav, c.boxes, c.diffuse, c.glossy, c.glass,
+                                          c.sun, c.samples};
 #pragma unroll
         for (int q = 0; q < NCOUNTS; ++q) {
             unsigned long long x = v[q];
@@ -1099,7 +1119,7 @@ __device__ __forceinline__ bool fast_round(const DevScene& S, FastRay& R, const 
                                            const LaneStack& st, unsigned kstride, Cnt& c) {
     const unsigned sstride = st.stride;
     while (R.item >= 0) {
-        if (COUNT) { count_wave(c.wave_trav); c.nodes++; }
+        if (COUNT) { count_wave(c.wave_trav); c.nodes++; c.boxes += 2; }
         const char* np = nb + (SOA ? 16u : 16u * kNodeF4) * (unsigned)R.item;
         R.item = node_step<OVF>(np, kstride, R.o, R.ix, R.iy, R.iz, R.bk * CULL_MARGIN, st, R.soff);
     }
@@ -1147,7 +1167,7 @@ __device__ __forceinline__ bool fast_step(const DevScene& S, FastRay& R, const c
     const int2 e = *reinterpret_cast<const int2*>(p + (node ? 3 * ks : 0u));
     if (COUNT) count_wave(c.wave_trav);
     if (node) {
-        if (COUNT) c.nodes++;
+        if (COUNT) { c.nodes++; c.boxes += 2; }
         R.item = node_pick<OVF>(g0, g1, g2, e, R.o, R.ix, R.iy, R.iz, R.bk * CULL_MARGIN, st, R.soff);
         if (R.item != INT_MIN) return false;
     } else {
@@ -1185,7 +1205,7 @@ __global__ void __launch_bounds__(256) render_resume_kernel(DevScene S, FramePar
                                                       const LaunchConst* __restrict__ lconst) {
     extern __shared__ int lds_stack[];
     const int B = blockDim.x;
-    Cnt c{0, 0, 0, 0, 0, 0, 0, 0, 0};
+    Cnt c{};
     const LaunchConst& C = *lconst;
     const float4* nodes = S.nodes;
     const float4* tris = S.tri_fast;
@@ -1235,6 +1255,7 @@ __global__ void __launch_bounds__(256) render_resume_kernel(DevScene S, FramePar
     auto finish_sample = [&]() __attribute__((always_inline)) {  // output += baseColor; next sample from the cached camera hit
         if (LOG && logme) log_event(F, 3.0f, s + 1, rtm_v3(0, 0, 0), rtm_v3(0, 0, 0), 0.0f, 0, so);
         acc = rtm_add(acc, so);
+        if (COUNT) c.samples++;
         ++s;
         if (s >= spp) write_pixel();
         // the next sample restarts from the cached camera hit; written as selects so that no branch
@@ -1332,6 +1353,7 @@ __global__ void __launch_bounds__(256) render_resume_kernel(DevScene S, FramePar
                     log_event(F, 2.0f, j, Bo, C.sun, h.tri >= 0 ? h.k : -1.0f, hm, so);
                 }
                 rtm_f3 sunLight = rtm_v3(0, 0, 0);
+                if (COUNT) c.sun++;
                 const Mat cm = load_mat(S.mat, __float_as_int(S.tri_shade[tri].w));
                 if (h.tri < 0 && cm.type != 3) sunLight = rtm_v3(e3, e3, e3);
                 if (h.tri >= 0) {
@@ -1361,6 +1383,7 @@ __global__ void __launch_bounds__(256) render_resume_kernel(DevScene S, FramePar
                         const rtm_f3 nn = xyz(f2);
                         float invPdf = 0.0f;
                         rtm_f3 brdf = rtm_v3(0, 0, 0);
+                        if (COUNT) count_event(c, cm.type);
                         if (cm.type == 1) {
                             Bd = hemi_cosine(n, S.tri_frame[3 * tri], S.tri_frame[3 * tri + 1], f2, &seed1, &seed0,
                                              &invPdf);
@@ -1403,7 +1426,8 @@ __global__ void __launch_bounds__(256) render_resume_kernel(DevScene S, FramePar
     }
     if (COUNT) {
         unsigned long long v[NCOUNTS] = {c.nodes, c.tris, c.rays, c.env, c.dropped, c.wave_trav, c.wave_outer,
-                                          c.cyc_shade, c.cyc_trav};
+                                          c.cyc_shade, c.cyc_trav, c.boxes, c.diffuse, c.glossy, c.glass,
+                                          c.sun, c.samples};
 #pragma unroll
         for (int q = 0; q < NCOUNTS; ++q) {
             unsigned long long x = v[q];
@@ -1541,7 +1565,7 @@ __global__ void __launch_bounds__(256) debug_trace_kernel(DevScene S, const floa
     extern __shared__ int lds_stack[];
     const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= n) return;
-    Cnt c{0, 0, 0, 0, 0, 0, 0, 0, 0};
+    Cnt c{};
     const float* r = rays + 6 * t;
     const Hit h = trace<TRAV, false>(S, S.nodes, S.tri_fast, rtm_v3(r[3], r[4], r[5]), rtm_v3(r[0], r[1], r[2]),
                                      lds_stack + threadIdx.x, blockDim.x, lane_stack(S, lds_stack), c);

@@ -117,6 +117,18 @@ int64_t rt_tile_rows(int64_t npix, int width, int row0, int row_step);
 int rt_count_work(rt_ctx* ctx, const float cam[10], const float env[5], int64_t npix, int spp,
                   int max_bounce, int row0, int row_step, uint64_t counts[5]);
 
+/* Every counter of the instrumented render of the tile (device 0, blocking):
+ * counts[0..4] as rt_count_work, [5] traversal-loop iterations per wave,
+ * [6] render-loop iterations per wave, [7]/[8] clock cycles the resumable
+ * kernel's waves spend shading / traversing, [9] ray-box slab tests (a FAST
+ * node tests 2 boxes, a REF node 1, the brute-force path one per distinct
+ * leaf box), [10]/[11]/[12] shading events (naiveGI bounces,
+ * Raytracing.cl:58-78) on materials of type 1 (diffuse) / 2 (glossy) /
+ * 3 (glass), [13] sun terms evaluated (Raytracing.cl:115-137), [14] samples,
+ * [15] 0.  Feeds the VALU roofline of bench.py. */
+int rt_count_work_detail(rt_ctx* ctx, const float cam[10], const float env[5], int64_t npix, int spp,
+                         int max_bounce, int row0, int row_step, uint64_t counts[16]);
+
 /* Algorithmic bytes per unit of the counters above:
  * out[0] = per node fetch (32 B per box tested: 64 for a FAST node, which
  * tests both children; 32 for a REF node), out[1] = 36 per triangle test,

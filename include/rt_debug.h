@@ -37,8 +37,10 @@ int rt_debug_wave_counts(rt_ctx* ctx, const float cam[10], const float env[5], i
                          int max_bounce, uint64_t out[9]);
 
 /* Scene facts: out[0] = FAST layout available (1/0), out[1] = FAST stack
- * depth, out[2] = internal nodes, out[3] = triangles. */
-int rt_debug_scene_info(rt_ctx* ctx, int64_t out[4]);
+ * depth, out[2] = internal nodes, out[3] = triangles, out[4] = brute-force
+ * records (0: the tree walk renders), out[5] = distinct leaf boxes of the
+ * brute-force path, out[6], out[7] = 0. */
+int rt_debug_scene_info(rt_ctx* ctx, int64_t out[8]);
 
 #ifdef __cplusplus
 }

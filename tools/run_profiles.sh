@@ -1,13 +1,25 @@
 #!/bin/bash
-# rocprofv3 passes for the benchmark workload (run on the GPU box from the repo root).
-# Kernel trace + stats in one run; each PMC counter group in its own run (no sys/runtime trace).
+# rocprofv3 passes of bench.py for one workload (run on the GPU box from the repo root):
+#   tools/run_profiles.sh OUTDIR CONFIG [extra bench.py args]
+# One kernel-trace + stats run, then each PMC counter group in its own run (no sys/runtime trace,
+# at most 8 SQ / 4 TCC / 2 GRBM counters per pass).  Summarise with tools/summarize_profiles.py.
 set -euo pipefail
 export TMPDIR=/tmp
-OUT=${1:-gpurun_out/prof}
-ARGS=${BENCH_ARGS:-"--steps 10 --warmup 2 --no-cpu-baseline"}
+OUT=$1
+CFG=$2
+shift 2
+ARGS="--config $CFG --no-cpu-baseline --no-extra $*"
 mkdir -p "$OUT"
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/kt" -o kt -- python3 bench.py $ARGS > "$OUT/kt.log" 2>&1
-timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/fetch" -o fetch -- python3 bench.py $ARGS > "$OUT/fetch.log" 2>&1
-timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/write" -o write -- python3 bench.py $ARGS > "$OUT/write.log" 2>&1
-timeout -k 10 300 rocprofv3 --pmc TCC_EA0_RDREQ_DRAM_sum TCC_EA0_WRREQ_DRAM_sum --output-format csv -d "$OUT/dram" -o dram -- python3 bench.py $ARGS > "$OUT/dram.log" 2>&1
-echo profiles done
+run() {
+  local name=$1
+  shift
+  echo "pass $name"
+  timeout -s KILL "${PASS_TIMEOUT:-300}" rocprofv3 "$@" --output-format csv -d "$OUT/$name" -o "$name" -- \
+    python3 bench.py $ARGS > "$OUT/$name.log" 2>&1
+}
+run kt --kernel-trace --stats
+run fetch --pmc FETCH_SIZE
+run write --pmc WRITE_SIZE
+run dram --pmc TCC_EA0_RDREQ_DRAM_sum TCC_EA0_WRREQ_DRAM_sum TCC_EA0_WRREQ_64B_sum
+run sq --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_THREAD_CYCLES_VALU SQ_WAIT_ANY SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE GRBM_COUNT
+echo "profiles of $CFG done"

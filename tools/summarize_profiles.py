@@ -1,17 +1,21 @@
-"""Summarise rocprofv3 output of tools/run_profiles.sh into profiles/ (committed evidence).
+"""Summarise the rocprofv3 output of tools/run_profiles.sh into profiles/ (committed evidence).
 
-    python tools/summarize_profiles.py gpurun_out/prof TAG WORKLOAD
+    python tools/summarize_profiles.py gpurun_out/prof_C2 TAG WORKLOAD
 
-Writes profiles/TAG_kernel_stats_WORKLOAD.csv (the --stats table of the kernel-trace run)
-and profiles/TAG_pmc_WORKLOAD.json: per-launch counters of the render kernel and the HBM
-bytes per launch, corrected as MI355X_MICROARCH.md prescribes for gfx950 (FETCH_SIZE is in
-KiB and reads 1/2 of a wide streaming read's bytes -> x2; WRITE_SIZE in KiB, exact).
+Writes profiles/TAG_kernel_stats_WORKLOAD.csv (the --stats table of the kernel-trace run) and
+profiles/TAG_pmc_WORKLOAD.json: per-launch means of every counter of the render kernel, and
+  hbm_bytes_per_launch = (2 x FETCH_SIZE + WRITE_SIZE) KiB -> bytes, corrected as
+      MI355X_MICROARCH.md prescribes for gfx950 (FETCH_SIZE counts half of a wide read's bytes;
+      WRITE_SIZE exact);
+  valu_lane_slots_per_launch = SQ_INSTS_VALU x 64 (wave-level VALU instructions x lanes);
+  valu_lane_util = SQ_THREAD_CYCLES_VALU / (64 x SQ_ACTIVE_INST_VALU) (active lanes per VALU issue);
+  valu_issue_frac = valu_lane_slots_per_launch / kernel time / 78.64e12 lane-ops/s.
 """
 import csv
-import re
 import glob
 import json
 import os
+import re
 import shutil
 import sys
 
@@ -32,28 +36,38 @@ def _rows(pattern):
 def main(prof, tag, workload, kernel=KERNEL):
     os.makedirs(os.path.join(ROOT, "profiles"), exist_ok=True)
     stats = glob.glob(os.path.join(prof, "kt", "*kernel_stats.csv"))
-    summary = {"workload": workload, "kernel": kernel, "source": "rocprofv3 (tools/run_profiles.sh)"}
+    s = {"workload": workload, "kernel": kernel, "source": "rocprofv3 (tools/run_profiles.sh)"}
     if stats:
         shutil.copy(stats[0], os.path.join(ROOT, "profiles", f"{tag}_kernel_stats_{workload}.csv"))
         for r in _rows(stats[0]):
             if re.search(kernel, r["Name"]):
-                summary["kernel_calls"] = int(r["Calls"])
-                summary["kernel_avg_ms"] = float(r["AverageNs"]) / 1e6
+                s["kernel_name"] = r["Name"][:120]
+                s["kernel_calls"] = int(r["Calls"])
+                s["kernel_avg_ms"] = float(r["AverageNs"]) / 1e6
     counters = {}
-    for sub in ("fetch", "write", "dram"):
+    for sub in ("fetch", "write", "dram", "sq"):
         for r in _rows(os.path.join(prof, sub, "*counter_collection.csv")):
             if re.search(kernel, r["Kernel_Name"]):
                 counters.setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))
-    for k, v in counters.items():
-        summary[k + "_per_launch"] = float(np.mean(v))
-        summary[k + "_launches"] = len(v)
-    if "FETCH_SIZE_per_launch" in summary and "WRITE_SIZE_per_launch" in summary:
-        summary["hbm_bytes_per_launch"] = (2.0 * summary["FETCH_SIZE_per_launch"] + summary["WRITE_SIZE_per_launch"]) * 1024
-        summary["hbm_bytes_note"] = ("FETCH_SIZE x2 (gfx950 half-count correction for wide reads; this kernel's "
-                                     "narrow gathers are uncalibrated) + WRITE_SIZE, KiB -> bytes")
+    for k, v in sorted(counters.items()):
+        s[k + "_per_launch"] = float(np.mean(v))
+        s[k + "_launches"] = len(v)
+    g = lambda k: s.get(k + "_per_launch")  # noqa: E731
+    if g("FETCH_SIZE") is not None and g("WRITE_SIZE") is not None:
+        s["hbm_bytes_per_launch"] = (2.0 * g("FETCH_SIZE") + g("WRITE_SIZE")) * 1024
+        s["hbm_bytes_note"] = "(2 x FETCH_SIZE + WRITE_SIZE) KiB: gfx950 half-count correction of FETCH_SIZE"
+        if s.get("kernel_avg_ms"):
+            s["hbm_GBps"] = s["hbm_bytes_per_launch"] / (s["kernel_avg_ms"] * 1e-3) / 1e9
+            s["hbm_frac_of_8TBps"] = s["hbm_GBps"] / 8000.0
+    if g("SQ_INSTS_VALU") is not None:
+        s["valu_lane_slots_per_launch"] = 64.0 * g("SQ_INSTS_VALU")
+        if g("SQ_ACTIVE_INST_VALU"):
+            s["valu_lane_util"] = g("SQ_THREAD_CYCLES_VALU") / (64.0 * g("SQ_ACTIVE_INST_VALU"))
+        if s.get("kernel_avg_ms"):
+            s["valu_issue_frac"] = s["valu_lane_slots_per_launch"] / (s["kernel_avg_ms"] * 1e-3) / 78.6432e12
     with open(os.path.join(ROOT, "profiles", f"{tag}_pmc_{workload}.json"), "w") as f:
-        json.dump(summary, f, indent=1)
-    print(json.dumps(summary, indent=1))
+        json.dump(s, f, indent=1)
+    print(json.dumps(s, indent=1))
 
 
 if __name__ == "__main__":
