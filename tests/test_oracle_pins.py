@@ -116,3 +116,19 @@ def test_outpng_channel_means_rows():
     mine = img.reshape(-1, 3).mean(0) / 255.0
     ref = z["row_means"][0::8].mean(0) / 255.0
     np.testing.assert_allclose(mine, ref, rtol=5e-3)
+
+
+def test_oracle_drops_pushes_beyond_the_reference_stack():
+    """The oracle's REF traversal reproduces stack.cl's silent drop on a BVH deeper than 20
+    levels (tests/deep_bvh.py): pushes are dropped, and the nearest triangle (in a dropped
+    subtree) is never tested, so a straight-on camera ray hits a farther one."""
+    from tests.deep_bvh import caterpillar_scene
+    arr = caterpillar_scene(40)
+    ibl = np.zeros((2, 2, 4), np.uint8)
+    osc = O.OracleScene(arr["V_p"], arr["V_n"], arr["V_uv"], arr["faceData"], arr["materialData"], arr["bvh"], ibl)
+    cam = np.array([0, -3.5, 0, 0, 0, 0, 16, 16, 1, 45 * 3.14 / 180], np.float32)
+    env = np.array([90, 0, 0, 1.0, 1.0], np.float32)
+    _, c = O.render(osc, cam, env, 256, 1, 0, nthreads=2, counts=True)
+    assert c["dropped"] > 0
+    hit = O.trace(osc, np.array([0, 1, 0, 0, -3.5, 0], np.float32))   # out: n.xyz, k, mat, bHit
+    assert hit[5] == 1 and hit[3] > 5.0   # a hit, but not the nearest triangle (at distance 4.5)

@@ -170,3 +170,43 @@ def test_native_obj_parse_grid1m_matches_python():
     nat = _native.parse_obj(text)
     for a, b in zip(py[:4], nat[:4]):
         assert _same(a, b)
+
+
+# ---- the reference importer's own arrays (tests/golden/ref_scene_arrays.json, made by
+# tools/gen_scene_fixtures.py from FileManager.Scene in the reference checkout) ----
+REF_SCENES = os.path.join(os.path.dirname(__file__), "golden", "ref_scene_arrays.json")
+
+
+def _digest(a):
+    a = np.ascontiguousarray(a)
+    return {"dtype": str(a.dtype), "size": int(a.size), "sha256": hashlib.sha256(a.tobytes()).hexdigest()}
+
+
+@pytest.mark.parametrize("name", ["cornell", "monkey", "serre", "proto", "furnace"])
+def test_scene_arrays_match_the_reference_importer(name):
+    """faceData (uv, n, p order; u-line material counting, FileManager.py:253-291), materialData
+    (.ini M_* keys in file order, :309-324), lightData (:234-240), vertex arrays and the main.py
+    cam / envData packing (main.py:59-61, 72-73): bit for bit what the reference emits."""
+    with open(REF_SCENES) as f:
+        ref = json.load(f)["scenes"][name]
+    sc = W.load_scene(name)
+    for k in ("V_p", "V_n", "V_uv", "faceData", "materialData", "lightData"):
+        got = _digest(getattr(sc, k))
+        want = {kk: ref[k][kk] for kk in ("dtype", "size", "sha256")}
+        assert got == want, (name, k)
+    np.testing.assert_array_equal(sc.materialData, np.array(ref["materialData"]["values"], np.float32))
+    assert sc.materialCount == ref["materialCount"]
+    assert sc.camera().view(np.uint32).tolist() == ref["cam_bits"]
+    assert sc.env().view(np.uint32).tolist() == ref["env_bits"]
+
+
+def test_grid1m_obj_and_bvh_hashes():
+    """SURVEY App. D grid-1M (C5): OBJ text and BVH.py export pinned by their hashes (native builder)."""
+    with open(HASHES) as f:
+        h = json.load(f)["grid1m"]
+    text = W.grid_obj_text(708)
+    assert hashlib.sha256(text.encode()).hexdigest()[:16] == h["obj_sha256_16"]
+    sc = W.grid_scene(708)
+    arr = sc.BVH.exportArray
+    assert arr.size // 9 == h["nodes"] == 2_005_055
+    assert hashlib.sha256(arr.tobytes()).hexdigest()[:16] == h["sha256_16"]
