@@ -197,6 +197,9 @@ def main():
     ap.add_argument("--traversal", default="fast", choices=["fast", "ref"])
     ap.add_argument("--bvh", default="sah", choices=["sah", "reference"])
     ap.add_argument("--block", type=int, default=0)
+    ap.add_argument("--option", action="append", default=[], help="rt_set_option KEY=VALUE (repeatable)")
+    ap.add_argument("--bvh-width", type=int, default=0, choices=[0, 2, 4],
+                    help="FAST tree walk layout: 2 = BVH2, 4 = 4-wide quantised (0 = library default)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extra", action="store_true", help="skip the C3/C4 lines and the host-boundary timing")
     ap.add_argument("--check", action="store_true",
@@ -232,6 +235,11 @@ def main():
         c.set_option("bvh", _native.RT_BVH_SAH if args.bvh == "sah" else _native.RT_BVH_REFERENCE)
         if args.block:
             c.set_option("block", args.block)
+        if args.bvh_width:
+            c.set_option("bvh_width", args.bvh_width)
+        for kv in args.option:
+            k, v = kv.split("=")
+            c.set_option(k, int(v))
         return c
 
     wl = Wk.CONFIGS[args.config]

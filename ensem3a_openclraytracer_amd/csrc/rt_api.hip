@@ -46,7 +46,7 @@ struct Device {
     hipStream_t stream = nullptr;
     int cus = 0;                  // compute units (sizes the FAST stack overflow buffer)
     DevBuf stack_ovf;             // FAST traversal stack entries beyond the LDS part
-    DevBuf nodes, tri_fast, brute, brute_box, bvh9, tri_geo, tri_shade, tri_frame, mat, ibl, out, out8, counts, work, scratch_a, scratch_b;
+    DevBuf nodes, wnodes, wleaves, tri_fast, brute, brute_box, bvh9, tri_geo, tri_shade, tri_frame, mat, ibl, out, out8, counts, work, scratch_a, scratch_b;
     char* host_stage = nullptr;   // pinned staging for rt_render / rt_render_rgb8
     size_t host_stage_bytes = 0;
     // Every launch of this context on the device shares `work` (pixel counters + launch constants)
@@ -61,6 +61,9 @@ struct Device {
 // Host copy of the packed scene (kept to upload on every device).
 struct HostScene {
     std::vector<float> nodes;      // 16 floats per internal node
+    std::vector<float> wnodes;     // wide layout: 16 floats per 4-wide node (DevScene::wnodes)
+    std::vector<float> wleaves;    // wide layout: 16 floats per leaf, in reference DFS rank order
+    int32_t nwnodes = 0, wroot_ref = 0, wdepth = 1;
     std::vector<float> bvh9;
     std::vector<float> tri_geo;    // 12 floats per triangle
     std::vector<float> tri_fast;   // tri_geo's records in FAST leaf order (DevScene::tri_fast)
@@ -95,6 +98,8 @@ struct rt_ctx {
     int sun_skip = 1;   // FAST: do not trace shadow rays of an unlit sun (FrameParams::sun_skip)
     int sun_any = 1;    // FAST tree walk: shadow rays end at their first hit when no material is glass
     int block = 128;
+    int shade_sort = 0; // resumable walk: one material type shaded per wave iteration (FrameParams::shade_sort)
+    int bvh_width = 0;  // FAST tree walk: 2 = BVH2 nodes, 4 = the 4-wide quantised layout, 0 = auto (option "bvh_width")
     std::string err;
 };
 
@@ -157,6 +162,144 @@ inline bool fidx(float v, int64_t limit, int32_t* out) {
     if (i < -1 || i >= limit) return false;
     *out = i;
     return true;
+}
+
+// p + q * s in fp32 (q * s is exact: s is a power of two): a quantised box bound, exactly as the
+// kernels dequantise it (rt_kernels.hip wide_step; this file is built with -ffp-contract=off).
+inline float deq(float p, uint32_t q, float s) { return p + (float)q * s; }
+
+// Per-axis quantisation of up to 4 child boxes against their union's lower corner p: a scale
+// 2^e and byte bounds whose dequantised box contains each child's exact box.  Returns the
+// biased exponent byte (scale = as_float(e << 23)).
+uint32_t quantise_axis(float p, const float* lo, const float* hi, int n, uint8_t* qlo, uint8_t* qhi) {
+    double ext = 0.0;
+    for (int c = 0; c < n; ++c) ext = std::max(ext, (double)hi[c] - (double)p);
+    int e = ext > 0.0 ? (int)std::ceil(std::log2(ext / 255.0)) : -100;
+    e = std::min(std::max(e, -100), 100);
+    for (;; ++e) {
+        const float sc = std::ldexp(1.0f, e);
+        bool ok = true;
+        for (int c = 0; c < n && ok; ++c) {
+            double fl = std::floor(((double)lo[c] - p) / sc), fh = std::ceil(((double)hi[c] - p) / sc);
+            uint32_t a = (uint32_t)std::min(255.0, std::max(0.0, fl));
+            uint32_t b = (uint32_t)std::min(255.0, std::max(0.0, fh));
+            while (a > 0 && deq(p, a, sc) > lo[c]) --a;
+            while (b < 255 && deq(p, b, sc) < hi[c]) ++b;
+            ok = deq(p, a, sc) <= lo[c] && deq(p, b, sc) >= hi[c];
+            qlo[c] = (uint8_t)a;
+            qhi[c] = (uint8_t)b;
+        }
+        if (ok || e >= 100) return (uint32_t)(e + 127);
+    }
+}
+
+// Wide layout of the FAST tree (DevScene::wnodes / wleaves, option "bvh_width" 4): the binary tree
+// collapsed to nodes of up to 4 children (the internal child with the largest surface area is
+// replaced by its two children while fewer than 4), BFS order, 64 bytes per node:
+//   float4 (p.x, p.y, p.z, exponent bytes ex | ey << 8 | ez << 16)    p = the children's lower corner
+//   int4   child refs: >= 0 wide node, < 0 leaf ~(64 * rank), INT_MIN = empty slot
+//   uint4  (lo.x, lo.y, lo.z, hi.x), uint4 (hi.y, hi.z, 0, 0): one byte per child per word
+// A child box dequantises per axis as p + q * 2^(e-127), a superset of the child's exact box, so an
+// internal child is never rejected where its leaves would pass.  Leaves, one triangle each, are
+// 64-byte records in the reference's DFS rank order (rank = record index, the tie break):
+// exact leaf box lo.xyz hi.x | hi.yz a.xy | a.z e1.xyz | e2.xyz triangle index.  The leaf step
+// tests the exact box again, so the accepted triangles are those of the binary walk.
+void emit_wide(HostScene& hs, const int32_t* L, const int32_t* R, const int32_t* T, const float* box, int64_t nn) {
+    hs.wnodes.clear();
+    hs.wleaves.clear();
+    hs.nwnodes = 0;
+    hs.wroot_ref = 0;
+    hs.wdepth = 1;
+    if (hs.ntri > (1 << 25)) return;   // leaf refs ~(64 * rank) must fit 31 bits: no wide layout
+    auto is_inner = [&](int64_t i) { return L[i] >= 0; };
+    auto area = [&](int64_t i) {
+        const float* b = box + 6 * i;
+        const double x = (double)b[3] - b[0], y = (double)b[4] - b[1], z = (double)b[5] - b[2];
+        return x * y + y * z + z * x;
+    };
+    auto kids = [&](int32_t n) {
+        std::vector<int32_t> k{L[n], R[n]};
+        while (k.size() < 4) {
+            int best = -1;
+            for (int i = 0; i < (int)k.size(); ++i)
+                if (is_inner(k[i]) && (best < 0 || area(k[i]) > area(k[best]))) best = i;
+            if (best < 0) break;
+            const int32_t c = k[best];
+            k[best] = L[c];
+            k.insert(k.begin() + best + 1, R[c]);
+        }
+        return k;
+    };
+    auto rank_of = [&](int32_t leaf) { return as_i32(hs.tri_geo[12 * (size_t)T[leaf] + 3]); };
+    std::vector<int32_t> wide_of(nn, -1), bfs;
+    std::vector<std::vector<int32_t>> children;
+    if (is_inner(0)) {
+        bfs.push_back(0);
+        wide_of[0] = 0;
+    }
+    for (size_t h = 0; h < bfs.size(); ++h) {
+        children.push_back(kids(bfs[h]));
+        for (int32_t ch : children.back()) {
+            if (!is_inner(ch)) continue;
+            wide_of[ch] = (int32_t)bfs.size();
+            bfs.push_back(ch);
+        }
+    }
+    std::vector<int32_t> need(bfs.size(), 0);
+    for (size_t w = bfs.size(); w-- > 0;) {
+        int32_t sub = 0;
+        for (int32_t ch : children[w])
+            if (is_inner(ch)) sub = std::max(sub, need[wide_of[ch]]);
+        need[w] = (int32_t)children[w].size() - 1 + sub;
+    }
+    hs.nwnodes = (int32_t)bfs.size();
+    hs.wnodes.assign((size_t)hs.nwnodes * 16, 0.0f);
+    int32_t nleaves = 0;
+    for (int64_t i = 0; i < nn; ++i)
+        if (!is_inner(i) && T[i] >= 0) nleaves = std::max(nleaves, rank_of((int32_t)i) + 1);
+    hs.wleaves.assign((size_t)std::max(nleaves, 1) * 16, 0.0f);
+    auto leaf_ref = [&](int32_t c) { return ~(64 * rank_of(c)); };
+    for (size_t w = 0; w < bfs.size(); ++w) {
+        float* o = hs.wnodes.data() + 16 * w;
+        const auto& ch = children[w];
+        const int n = (int)ch.size();
+        float lo[3][4], hi[3][4];
+        float p[3];
+        for (int a = 0; a < 3; ++a) {
+            p[a] = INFINITY;
+            for (int c = 0; c < n; ++c) {
+                lo[a][c] = box[6 * (int64_t)ch[c] + a];
+                hi[a][c] = box[6 * (int64_t)ch[c] + 3 + a];
+                p[a] = std::min(p[a], lo[a][c]);
+            }
+        }
+        uint8_t ql[3][4] = {}, qh[3][4] = {};
+        uint32_t meta = 0;
+        for (int a = 0; a < 3; ++a) meta |= quantise_axis(p[a], lo[a], hi[a], n, ql[a], qh[a]) << (8 * a);
+        o[0] = p[0]; o[1] = p[1]; o[2] = p[2]; o[3] = as_f32((int32_t)meta);
+        for (int c = 0; c < 4; ++c)
+            o[4 + c] = as_f32(c < n ? (is_inner(ch[c]) ? wide_of[ch[c]] : leaf_ref(ch[c])) : INT32_MIN);
+        auto pack = [&](const uint8_t* q) {
+            uint32_t v = 0;
+            for (int c = 0; c < 4; ++c) v |= (uint32_t)q[c] << (8 * c);
+            return as_f32((int32_t)v);
+        };
+        o[8] = pack(ql[0]); o[9] = pack(ql[1]); o[10] = pack(ql[2]); o[11] = pack(qh[0]);
+        o[12] = pack(qh[1]); o[13] = pack(qh[2]); o[14] = 0.0f; o[15] = 0.0f;
+    }
+    for (int64_t i = 0; i < nn; ++i) {
+        if (is_inner(i) || T[i] < 0) continue;
+        const int32_t r = rank_of((int32_t)i);
+        float* q = hs.wleaves.data() + 16 * (size_t)r;
+        const float* b = box + 6 * i;
+        const float* g = hs.tri_geo.data() + 12 * (size_t)T[i];
+        q[0] = b[0]; q[1] = b[1]; q[2] = b[2]; q[3] = b[3];
+        q[4] = b[4]; q[5] = b[5]; q[6] = g[0]; q[7] = g[1];
+        q[8] = g[2]; q[9] = g[4]; q[10] = g[5]; q[11] = g[6];
+        q[12] = g[8]; q[13] = g[9]; q[14] = g[10]; q[15] = as_f32(T[i]);
+    }
+    hs.wroot_ref = is_inner(0) ? 0 : leaf_ref(0);
+    hs.wdepth = bfs.empty() ? 1 : std::max(1, need[0]);
 }
 
 // Emit the FAST node array from a binary tree with one triangle per leaf: internal nodes in BFS
@@ -229,6 +372,7 @@ void emit_bvh(HostScene& hs, const int32_t* L, const int32_t* R, const int32_t* 
     hs.root_ref = is_inner(0) ? 0 : ~(48 * pos[T[0]]);
     for (int k = 0; k < 6; ++k) hs.root_box[k] = box[k];
     hs.depth = bfs.empty() ? 1 : std::max(1, need[0]);
+    emit_wide(hs, L, R, T, box, nn);
 }
 
 // Pack the FAST layout from the reference export.  Returns false (with
@@ -392,9 +536,11 @@ void pack_checked(HostScene& hs, const float* bvh9, int64_t nb, int64_t ntri, in
     hs.fast_ok = (ntri > 0) ? pack_fast(hs, bvh9, nb, ntri, layout, brute_max, why) : true;
     if (ntri == 0) {
         hs.nnodes = 0; hs.root_ref = 0; hs.depth = 1; hs.nodes.clear();
+        hs.nwnodes = 0; hs.wroot_ref = 0; hs.wdepth = 1; hs.wnodes.clear(); hs.wleaves.clear();
         hs.brute.clear(); hs.brute_box.clear(); hs.nbrute = 0; hs.nbox = 0;
     }
     if (!hs.fast_ok) { hs.brute.clear(); hs.brute_box.clear(); hs.nbrute = 0; hs.nbox = 0; }
+    if (!hs.fast_ok || hs.wdepth > 64) { hs.wnodes.clear(); hs.wleaves.clear(); hs.nwnodes = 0; hs.wdepth = 1; }
     // render kernels keep kStackLds entries in LDS and spill deeper ones to HBM; the single-ray
     // debug kernel keeps the whole stack in LDS (int2 entries, 128 lanes): depth <= 64
     if (hs.fast_ok && hs.depth > 64) {
@@ -409,7 +555,7 @@ void pack_checked(HostScene& hs, const float* bvh9, int64_t nb, int64_t ntri, in
 // HBM part of the FAST traversal stack: (depth - kStackLds) entries for every lane a
 // persistent render grid can hold.
 hipError_t ensure_stack_ovf(Device& d, const HostScene& hs) {
-    const int64_t extra = (int64_t)hs.depth - rt::kStackLds;
+    const int64_t extra = (int64_t)std::max(hs.depth, hs.wdepth) - rt::kStackLds;
     if (extra <= 0) return hipSuccess;
     return ensure(d.stack_ovf, (size_t)std::max(d.cus, 1) * rt::kMaxLanesPerCu * (size_t)extra * sizeof(int2));
 }
@@ -433,11 +579,22 @@ hipError_t upload(DevBuf& b, const std::vector<T>& v, hipStream_t s) {
     return hipMemcpyAsync(b.p, v.data(), bytes, hipMemcpyHostToDevice, s);
 }
 
+// The 4-wide layout serves the walk when chosen, or (auto) when the BVH2 node array exceeds
+// rt::kWideMinBytes.
+bool use_wide(const rt_ctx* ctx) {
+    if (ctx->hs.wnodes.empty() || ctx->bvh_width == 2) return false;
+    return ctx->bvh_width == 4 || (size_t)ctx->hs.nnodes * 16 * rt::kNodeF4 > rt::kWideMinBytes;
+}
+
 rt::DevScene dev_scene(const rt_ctx* ctx, const Device& d) {
     rt::DevScene s{};
     s.nodes = (const float4*)d.nodes.p;
     s.nnodes = ctx->hs.nnodes;
     s.root_ref = ctx->hs.root_ref;
+    const bool wide = use_wide(ctx);
+    s.wnodes = wide ? (const float4*)d.wnodes.p : nullptr;
+    s.wleaves = wide ? (const float4*)d.wleaves.p : nullptr;
+    s.wroot_ref = ctx->hs.wroot_ref;
     for (int k = 0; k < 6; ++k) s.root_box[k] = ctx->hs.root_box[k];
     s.bvh9 = (const float*)d.bvh9.p;
     s.nbvh9 = ctx->hs.nbvh9;
@@ -451,12 +608,14 @@ rt::DevScene dev_scene(const rt_ctx* ctx, const Device& d) {
     s.ibl = (const uchar4*)d.ibl.p;
     s.ibl_w = ctx->ibl_w;
     s.ibl_h = ctx->ibl_h;
-    s.depth = ctx->hs.depth;
+    // stack sized for whichever layout the launch picks (launch_fast uses the wide one only for the
+    // resumable walk of scenes not staged in LDS)
+    s.depth = wide ? std::max(ctx->hs.depth, ctx->hs.wdepth) : ctx->hs.depth;
     s.brute = (const float4*)d.brute.p;
     s.brute_box = (const float4*)d.brute_box.p;
     s.nbrute = ctx->hs.nbrute;
     s.nbox = ctx->hs.nbox;
-    s.stack_lds = std::min<int32_t>(ctx->hs.depth > 0 ? ctx->hs.depth : 1, rt::kStackLds);
+    s.stack_lds = std::min<int32_t>(s.depth > 0 ? s.depth : 1, rt::kStackLds);
     s.stack_ovf = (int2*)d.stack_ovf.p;
     return s;
 }
@@ -485,6 +644,8 @@ int check_frame(rt_ctx* ctx, const float* cam, const float* env, int64_t npix, i
     fp->step = ctx->step;
     fp->sun_skip = (ctx->sun_skip && env[3] == 0.0f && env[4] >= 0.0f && ctx->hs.colors_finite) ? 1 : 0;
     fp->sun_any = (ctx->sun_any && !ctx->hs.has_glass) ? 1 : 0;
+    fp->wide = use_wide(ctx) ? 1 : 0;
+    fp->shade_sort = ctx->shade_sort;
     fp->team = ctx->team;
     fp->max_waves = ctx->max_waves;
     fp->log_buf = nullptr;
@@ -544,7 +705,7 @@ void rt_destroy(rt_ctx* ctx) {
         if (hipSetDevice(d.id) != hipSuccess) continue;
         if (d.pending) (void)hipEventSynchronize(d.done);
         if (d.stream) (void)hipStreamSynchronize(d.stream);
-        for (DevBuf* b : {&d.stack_ovf, &d.nodes, &d.tri_fast, &d.brute, &d.brute_box, &d.bvh9, &d.tri_geo, &d.tri_shade, &d.tri_frame, &d.mat, &d.ibl, &d.out,
+        for (DevBuf* b : {&d.stack_ovf, &d.nodes, &d.wnodes, &d.wleaves, &d.tri_fast, &d.brute, &d.brute_box, &d.bvh9, &d.tri_geo, &d.tri_shade, &d.tri_frame, &d.mat, &d.ibl, &d.out,
                           &d.counts, &d.work, &d.scratch_a, &d.scratch_b})
             release(*b);
         if (d.host_stage) (void)hipHostFree(d.host_stage);
@@ -581,6 +742,8 @@ int rt_set_option(rt_ctx* ctx, const char* key, int64_t value) {
             HIP_OR_RET(ctx, hipSetDevice(d.id));
             HIP_OR_RET(ctx, order_after_last(d, d.stream));
             HIP_OR_RET(ctx, upload(d.nodes, hs.nodes, d.stream));
+            HIP_OR_RET(ctx, upload(d.wnodes, hs.wnodes, d.stream));
+            HIP_OR_RET(ctx, upload(d.wleaves, hs.wleaves, d.stream));
             HIP_OR_RET(ctx, upload(d.brute, hs.brute, d.stream));
             HIP_OR_RET(ctx, upload(d.brute_box, hs.brute_box, d.stream));
             HIP_OR_RET(ctx, upload(d.tri_geo, hs.tri_geo, d.stream));
@@ -620,6 +783,16 @@ int rt_set_option(rt_ctx* ctx, const char* key, int64_t value) {
     if (!std::strcmp(key, "waves")) {
         if (value < 0 || value > 8) return set_err(ctx, RT_ERR_ARG, "waves must be in 0..8");
         ctx->max_waves = (int)value;
+        return RT_OK;
+    }
+    if (!std::strcmp(key, "shade_sort")) {
+        if (value != 0 && value != 1) return set_err(ctx, RT_ERR_ARG, "shade_sort must be 0 or 1");
+        ctx->shade_sort = (int)value;
+        return RT_OK;
+    }
+    if (!std::strcmp(key, "bvh_width")) {
+        if (value != 0 && value != 2 && value != 4) return set_err(ctx, RT_ERR_ARG, "bvh_width must be 0 (auto), 2 or 4");
+        ctx->bvh_width = (int)value;
         return RT_OK;
     }
     if (!std::strcmp(key, "block")) {
@@ -719,6 +892,8 @@ int rt_set_scene(rt_ctx* ctx, const float* vp, int64_t nvp, const float* vn, int
         HIP_OR_RET(ctx, hipSetDevice(d.id));
         HIP_OR_RET(ctx, order_after_last(d, d.stream));
         HIP_OR_RET(ctx, upload(d.nodes, hs.nodes, d.stream));
+        HIP_OR_RET(ctx, upload(d.wnodes, hs.wnodes, d.stream));
+        HIP_OR_RET(ctx, upload(d.wleaves, hs.wleaves, d.stream));
         HIP_OR_RET(ctx, upload(d.brute, hs.brute, d.stream));
         HIP_OR_RET(ctx, upload(d.brute_box, hs.brute_box, d.stream));
         HIP_OR_RET(ctx, ensure_stack_ovf(d, hs));

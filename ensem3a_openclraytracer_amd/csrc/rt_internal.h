@@ -12,6 +12,10 @@ constexpr int kNodeF4 = 4;             // float4 per FAST BVH2 node (DevScene::n
 constexpr int kMaxLanesPerCu = 2048;   // resident threads per CU (gfx950)
 constexpr int kBoxGroup = 4;           // leaf boxes per scalar load group of the brute-force loop (DevScene::brute_box)
 constexpr int kMatF = 8;               // floats per device material row (DevScene::mat)
+// FAST tree walk over the 4-wide layout when the BVH2 node array exceeds this (option "bvh_width"
+// 0 = auto): trees that do not fit the L2, where the walk is bound by the latency of dependent
+// misses and half as many node fetches pay; smaller trees are bound by the item step's VALU.
+constexpr size_t kWideMinBytes = 16u << 20;
 
 // Per-launch scratch block (the `work` argument of launch_render): pixel hand-out counters of the
 // kGroups block groups (blockIdx.x % kGroups: the blocks one XCD runs under round-robin dispatch),
@@ -34,6 +38,12 @@ struct DevScene {
     const float4* nodes;
     int32_t nnodes;        // internal nodes in `nodes`
     int32_t root_ref;      // ref of the root (~(48 * tri) when the root is a leaf)
+    // the same tree collapsed to 4-wide nodes with quantised child boxes (rt_api.hip emit_wide):
+    // 64 bytes per node, 64-byte leaf records (exact leaf box + a.p, e1, e2 + index) in reference
+    // DFS rank order; refs >= 0 node, < 0 ~(64 * rank), INT_MIN empty slot
+    const float4* wnodes;
+    const float4* wleaves;
+    int32_t wroot_ref;
     float root_box[6];     // min.xyz, max.xyz of the root
     // REF traversal: the reference's own AoS export, 9 floats per node
     const float* bvh9;
@@ -90,6 +100,11 @@ struct FrameParams {
     // FAST tree walk: with no glass material the sun term depends only on whether the shadow ray hits
     // anything (Raytracing.cl:125-137), so its traversal ends at the first accepted triangle
     int32_t sun_any;
+    int32_t wide;        // FAST tree walk over the 4-wide quantised layout (DevScene::wnodes)
+    // resumable walk: material-coherent shading -- per render-loop iteration a wave shades the
+    // bounces of ONE material type (round robin over the types its lanes need); the other lanes
+    // wait one iteration (option "shade_sort")
+    int32_t shade_sort;
     // debug event log of one pixel (rt_debug_pixel_log only; unused by the product launches)
     int64_t log_pixel;
     float* log_buf;

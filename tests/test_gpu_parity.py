@@ -638,3 +638,42 @@ def test_full_size_c5_properties(kl):
     kl.native.render_device(cam, env, npix, spp, mb, 5, 97, t.data_ptr())
     torch.cuda.synchronize()
     np.testing.assert_array_equal(t.cpu().numpy(), f1.reshape(-1, W_ * 3)[5::97].reshape(-1))
+
+
+@pytest.mark.parametrize("case", ["monkey_c3_64_s4", "serre_96x54_s4", "proto_64_s4", "furnace_64_s4", "grid"])
+def test_wide_layout_renders_identically(kl, case):
+    """bvh_width 4: the tree collapsed to 4-wide nodes with 8-bit quantised child boxes (supersets of
+    the exact boxes) and leaf records carrying the exact leaf box -- the same accepted triangles,
+    so the same frame as the binary walk and the oracle (the grid case spills its stack to HBM)."""
+    if case == "grid":
+        sc, cam, env, npix, spp, mb, ibl = W.CONFIGS["C5"].with_size(48, 27, 2).inputs()
+    else:
+        sc, cam, env, npix, spp, mb, ibl = W.PARITY_CASES[case].inputs()
+    try:
+        kl.native.set_option("bvh_width", 4)
+        wide = _launch(kl, sc, cam, env, npix, spp, mb, ibl, "fast")
+        cw = kl.native.count_work_detail(cam, env, npix, spp, mb)
+        kl.native.set_option("bvh_width", 2)
+        narrow = _launch(kl, sc, cam, env, npix, spp, mb, ibl, "fast")
+        cn = kl.native.count_work_detail(cam, env, npix, spp, mb)
+    finally:
+        kl.native.set_option("bvh_width", 0)
+    np.testing.assert_array_equal(wide, narrow)
+    np.testing.assert_array_equal(wide, _oracle(sc, cam, env, npix, spp, mb, ibl))
+    assert cw["rays"] == cn["rays"] and cw["samples"] == cn["samples"]
+    assert cw["node_fetches"] < cn["node_fetches"]
+    with pytest.raises(_native.NativeError, match="bvh_width"):
+        kl.native.set_option("bvh_width", 8)
+
+
+@pytest.mark.parametrize("case", ["monkey_c3_64_s4", "serre_96x54_s4", "proto_64_s4"])
+def test_material_coherent_shading_renders_identically(kl, case):
+    """shade_sort: a wave shades one material type per iteration (round robin over the types its
+    lanes need) and the other lanes wait -- the per-lane event sequence, hence the frame, is unchanged."""
+    sc, cam, env, npix, spp, mb, ibl = W.PARITY_CASES[case].inputs()
+    try:
+        kl.native.set_option("shade_sort", 1)
+        got = _launch(kl, sc, cam, env, npix, spp, mb, ibl, "fast")
+    finally:
+        kl.native.set_option("shade_sort", 0)
+    np.testing.assert_array_equal(got, _oracle(sc, cam, env, npix, spp, mb, ibl))
