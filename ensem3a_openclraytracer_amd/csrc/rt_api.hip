@@ -98,7 +98,6 @@ struct rt_ctx {
     int sun_skip = 1;   // FAST: do not trace shadow rays of an unlit sun (FrameParams::sun_skip)
     int sun_any = 1;    // FAST tree walk: shadow rays end at their first hit when no material is glass
     int block = 128;
-    int shade_sort = 0; // resumable walk: one material type shaded per wave iteration (FrameParams::shade_sort)
     int bvh_width = 0;  // FAST tree walk: 2 = BVH2 nodes, 4 = the 4-wide quantised layout, 0 = auto (option "bvh_width")
     std::string err;
 };
@@ -645,7 +644,6 @@ int check_frame(rt_ctx* ctx, const float* cam, const float* env, int64_t npix, i
     fp->sun_skip = (ctx->sun_skip && env[3] == 0.0f && env[4] >= 0.0f && ctx->hs.colors_finite) ? 1 : 0;
     fp->sun_any = (ctx->sun_any && !ctx->hs.has_glass) ? 1 : 0;
     fp->wide = use_wide(ctx) ? 1 : 0;
-    fp->shade_sort = ctx->shade_sort;
     fp->team = ctx->team;
     fp->max_waves = ctx->max_waves;
     fp->log_buf = nullptr;
@@ -783,11 +781,6 @@ int rt_set_option(rt_ctx* ctx, const char* key, int64_t value) {
     if (!std::strcmp(key, "waves")) {
         if (value < 0 || value > 8) return set_err(ctx, RT_ERR_ARG, "waves must be in 0..8");
         ctx->max_waves = (int)value;
-        return RT_OK;
-    }
-    if (!std::strcmp(key, "shade_sort")) {
-        if (value != 0 && value != 1) return set_err(ctx, RT_ERR_ARG, "shade_sort must be 0 or 1");
-        ctx->shade_sort = (int)value;
         return RT_OK;
     }
     if (!std::strcmp(key, "bvh_width")) {

@@ -101,10 +101,6 @@ struct FrameParams {
     // anything (Raytracing.cl:125-137), so its traversal ends at the first accepted triangle
     int32_t sun_any;
     int32_t wide;        // FAST tree walk over the 4-wide quantised layout (DevScene::wnodes)
-    // resumable walk: material-coherent shading -- per render-loop iteration a wave shades the
-    // bounces of ONE material type (round robin over the types its lanes need); the other lanes
-    // wait one iteration (option "shade_sort")
-    int32_t shade_sort;
     // debug event log of one pixel (rt_debug_pixel_log only; unused by the product launches)
     int64_t log_pixel;
     float* log_buf;

@@ -1373,7 +1373,6 @@ __global__ void __launch_bounds__(256) render_resume_kernel(DevScene S, FramePar
 
     int phase = FETCH;
     bool tracing = false;
-    int last_type = 0;   // shade_sort: the material type this wave shaded last (wave-uniform)
     PixelQueue pq;
     FastRay T;
     T.item = 0; T.soff = 0; T.bk = 1000.0f; T.bt = -1; T.brank = -1; T.any = false;
@@ -1507,25 +1506,6 @@ __global__ void __launch_bounds__(256) render_resume_kernel(DevScene S, FramePar
                 so = rtm_mul(so, rtm_add(sunLight, envLight));
                 finish_sample();
             }
-            // material-coherent shading (FrameParams::shade_sort): the wave picks ONE material type,
-            // the next one after the last it shaded among those its waiting lanes need (ballots), and
-            // only bounces of that type are shaded now; a lane whose bounce has another type waits in
-            // PREP for a later iteration.  The per-lane sequence of events is unchanged.
-            int chosen = 0;
-            if (F.shade_sort) {
-                const int mt = (phase == PREP && j <= maxB && tri >= 0)
-                                   ? (int)S.mat[kMatF * __float_as_int(S.tri_shade[tri].w)] : 0;
-                const unsigned need_t = (__ballot(mt == 1) ? 2u : 0u) | (__ballot(mt == 2) ? 4u : 0u) |
-                                        (__ballot(mt == 3) ? 8u : 0u);
-                for (int q = 1; q <= 3 && need_t; ++q) {
-                    const int t = (last_type + q - 1) % 3 + 1;
-                    if ((need_t >> t) & 1u) {
-                        chosen = t;
-                        break;
-                    }
-                }
-                if (chosen) last_type = chosen;
-            }
             // naiveGI loop heads (Raytracing.cl:46-79) until a ray is needed or the pixel is done
             while (phase == PREP) {
                 if (j > maxB) {
@@ -1540,8 +1520,6 @@ __global__ void __launch_bounds__(256) render_resume_kernel(DevScene S, FramePar
                     if (cm.type == 0) {
                         so = rtm_scale(so, cm.rough);
                         finish_sample();
-                    } else if (F.shade_sort && cm.type != chosen) {
-                        break;   // shaded in a later iteration
                     } else {
                         const float4 f2 = S.tri_frame[3 * tri + 2];
                         const rtm_f3 nn = xyz(f2);

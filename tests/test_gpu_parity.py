@@ -665,15 +665,3 @@ def test_wide_layout_renders_identically(kl, case):
     with pytest.raises(_native.NativeError, match="bvh_width"):
         kl.native.set_option("bvh_width", 8)
 
-
-@pytest.mark.parametrize("case", ["monkey_c3_64_s4", "serre_96x54_s4", "proto_64_s4"])
-def test_material_coherent_shading_renders_identically(kl, case):
-    """shade_sort: a wave shades one material type per iteration (round robin over the types its
-    lanes need) and the other lanes wait -- the per-lane event sequence, hence the frame, is unchanged."""
-    sc, cam, env, npix, spp, mb, ibl = W.PARITY_CASES[case].inputs()
-    try:
-        kl.native.set_option("shade_sort", 1)
-        got = _launch(kl, sc, cam, env, npix, spp, mb, ibl, "fast")
-    finally:
-        kl.native.set_option("shade_sort", 0)
-    np.testing.assert_array_equal(got, _oracle(sc, cam, env, npix, spp, mb, ibl))
