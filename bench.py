@@ -121,7 +121,13 @@ def roofline(ctx, cnt: dict, kernel_ms: float, pixels: int, workload: str) -> di
     out["kernel_ms"] = round(kernel_ms, 4)
     out["path"] = (f"brute force ({info['brute_boxes']} distinct leaf boxes, {info['brute_records']} triangles)"
                    if brute else f"SAH tree walk ({info['nodes']} nodes, {info['tris']} triangles)")
-    out["other_bound"] = {"bound": "hbm" if brute else "valu", **other}
+    if brute:
+        # SURVEY 8(d)'s byte model charges HBM for records that this path reads from LDS and the scalar
+        # cache: reported as bytes only, never as a fraction of the HBM peak (it would exceed 1)
+        out["survey_bytes_model"] = {"alg_bytes_per_launch": hbm["alg_bytes_per_launch"],
+                                     "note": "records served from LDS / scalar cache, not HBM: no HBM fraction"}
+    else:
+        out["other_bound"] = {"bound": "valu", **other}
     out["counts_per_sample"] = {k: round(cnt[k] / max(1, cnt["samples"]), 4)
                                 for k in ("box_tests", "tri_tests", "rays", "ev_diffuse", "ev_glossy", "ev_glass",
                                           "sun_terms", "env_lookups", "node_fetches")}
