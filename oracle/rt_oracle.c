@@ -449,6 +449,32 @@ int oracle_pixel_log(const oracle_scene* sc, const float* cam, const float* env,
     return n;
 }
 
+/* One sample of pixel i as a function of its RNG offset: for every even offset D = 2p < 2P (draws
+ * consumed by the pixel's earlier samples), the sample's colour, the draws it consumes and the rays
+ * it traces.  A sample depends on nothing else (the primary hit is cached per pixel,
+ * Raytracing.cl:184-206), so the reference's pixel is the chain D0 = 0, D(k+1) = D(k) + draws(D(k))
+ * summed in order; tools/chain_speculation.py uses this to price sample-parallel speculation. */
+int oracle_sample_trail(const oracle_scene* sc, const float* cam, const float* env, int32_t npix, int32_t max_bounce,
+                        int32_t i, int32_t P, float* col, int32_t* draws, int32_t* rays) {
+    uint32_t a0 = (uint32_t)(i % npix), a1 = (uint32_t)(i / npix);
+    const ray r = genCameraRay(i, cam);
+    const hitInfo H = rayTrace(sc, r, NULL);
+    const material M = extractMaterial(sc->mat, H.mat);
+    for (int p = 0; p < P; ++p) {
+        uint32_t b0 = a0, b1 = a1;
+        oracle_counts cnt = {0, 0, 0, 0, 0};
+        const float3 o = naiveGI(rtm_v3(1.0f, 1.0f, 1.0f), max_bounce, H, r, M, sc, &b0, &b1, env, &cnt);
+        col[3 * p] = o.x; col[3 * p + 1] = o.y; col[3 * p + 2] = o.z;
+        rays[p] = (int32_t)cnt.rays;
+        uint32_t t0 = a0, t1 = a1;
+        int n = 0;   /* draws: steps of the (swapped-pointer) stream from the start state to the end state */
+        while (!(t0 == b0 && t1 == b1) && n < 4 * (max_bounce + 1) + 2) { rtm_rand(&t1, &t0); ++n; }
+        draws[p] = n;
+        rtm_rand(&a1, &a0); rtm_rand(&a1, &a0);
+    }
+    return 0;
+}
+
 /* ---- per-function known-answer hooks ---- */
 void oracle_rand_stream(uint32_t seed0, uint32_t seed1, int n, float* out, uint32_t* state_out) {
     for (int k = 0; k < n; ++k) out[k] = rtm_rand(&seed0, &seed1);

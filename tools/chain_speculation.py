@@ -1,0 +1,119 @@
+"""Price sample-parallel speculation for small tiles, on the CPU oracle.
+
+A pixel's samples form one chain: sample k starts at RNG offset D_k (draws consumed by samples
+0..k-1) and its colour and draw count are a function of D_k alone (the primary hit is cached,
+Raytracing.cl:184-206).  T lanes per pixel could run trails from guessed offsets G_t and stitch
+the chain where it lands on a computed offset (trails merge once they share an offset), keeping
+the frame bit-identical.  This script measures, per sampled pixel, the chain latency in traced
+rays for T = 1..4 with G_t = t * spp / T * mu (static guesses), against the serial chain.
+
+    python tools/chain_speculation.py [CONFIG] [PIXELS] [MU]
+"""
+import ctypes
+import heapq
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def trails(osc, cam, env, npix, mb, pixels, P):
+    import oracle.oracle as O
+    L = O.lib()
+    vp = ctypes.c_void_p
+    L.oracle_sample_trail.argtypes = [ctypes.POINTER(O._Scene), vp, vp, ctypes.c_int32, ctypes.c_int32,
+                                      ctypes.c_int32, ctypes.c_int32, vp, vp, vp]
+    out = []
+    for i in pixels:
+        col = np.zeros(3 * P, np.float32)
+        nd = np.zeros(P, np.int32)
+        nr = np.zeros(P, np.int32)
+        L.oracle_sample_trail(ctypes.byref(osc.c), cam.ctypes.data, env.ctypes.data, int(npix), int(mb), int(i),
+                              int(P), col.ctypes.data, nd.ctypes.data, nr.ctypes.data)
+        out.append((int(i), col.reshape(P, 3), nd, nr))
+    return out
+
+
+def chain(nd, spp):
+    D, seq = 0, []
+    for _ in range(spp):
+        seq.append(D)
+        if nd[D // 2] == 0:
+            seq += [D] * (spp - len(seq))
+            break
+        D += nd[D // 2]
+    return seq
+
+
+def speculate(nd, nr, spp, T, mu):
+    """Event simulation: lanes walk trails from G_t, a lane stops on an offset already computed or
+    being computed; returns (time the chain is complete, total rays traced) in rays."""
+    P = len(nd)
+    cost = lambda p: max(int(nr[p // 2]), 1)   # noqa: E731
+    done, claim, ev, work = {}, {}, [], 0
+    for t in range(T):
+        g = int(round(t * spp / T * mu / 2)) * 2
+        if g // 2 < P and g not in claim:
+            claim[g] = t
+            heapq.heappush(ev, (cost(g), t, g))
+    seq = chain(nd, spp)
+    tnow = 0
+    while ev:
+        tnow, t, p = heapq.heappop(ev)
+        done[p] = tnow
+        work += cost(p)
+        if all(q in done for q in seq):
+            return max(done[q] for q in seq), work
+        q = p + int(nd[p // 2])
+        if nd[p // 2] == 0 or q // 2 >= P or q in done or q in claim:
+            continue
+        claim[q] = t
+        heapq.heappush(ev, (tnow + cost(q), t, q))
+    tt = tnow
+    for q in seq:   # chain left every trail: finish it serially
+        if q not in done:
+            tt += cost(q)
+            work += cost(q)
+            done[q] = tt
+    return max(done[q] for q in seq), work
+
+
+def main():
+    import oracle.oracle as O
+    from ensem3a_openclraytracer_amd import workloads as W
+    name = sys.argv[1] if len(sys.argv) > 1 else "C2"
+    npx = int(sys.argv[2]) if len(sys.argv) > 2 else 400
+    mu = float(sys.argv[3]) if len(sys.argv) > 3 else 6.0
+    sc, cam, env, npix, spp, mb, ibl = W.CONFIGS[name].inputs()
+    osc = O.OracleScene.from_scene(sc, ibl)
+    cam = np.ascontiguousarray(cam, np.float32)
+    env = np.ascontiguousarray(env, np.float32)
+    P = spp * (mb + 1) + 64
+    pixels = np.random.default_rng(1).choice(npix, npx, replace=False)
+    tr = trails(osc, cam, env, npix, mb, pixels, P)
+    # the stitched chain reproduces the oracle's pixel bit for bit
+    W_ = int(cam[6])
+    for i, col, nd, nr in tr[:16]:
+        acc = np.zeros(3, np.float32)
+        for D in chain(nd, spp):
+            acc = acc + col[D // 2]
+        got = np.clip(acc / np.float32(spp), 0, 1).astype(np.float32)
+        ref = O.render(osc, cam, env, npix, spp, mb, row0=i // W_, row_step=npix).reshape(-1, 3)[i % W_]
+        assert np.array_equal(got, ref), i
+    ser = np.array([sum(max(int(nr[D // 2]), 1) for D in chain(nd, spp)) for _, _, nd, nr in tr])
+    mus = np.array([chain(nd, spp + 1)[-1] / spp for _, _, nd, _ in tr])
+    print(f"{name}: {npx} pixels, draws/sample mean {mus.mean():.2f} (std {mus.std():.2f}); serial chain "
+          f"mean {ser.mean():.1f} rays, max {ser.max()}")
+    for T in (2, 3, 4):
+        r = [speculate(nd, nr, spp, T, mu) for _, _, nd, nr in tr]
+        lat = np.array([a for a, _ in r], float)
+        wk = np.array([b for _, b in r], float)
+        print(f"T={T}: latency mean {lat.mean():.1f} p99 {np.percentile(lat, 99):.1f} max {lat.max():.0f} rays "
+              f"(max {ser.max() / lat.max():.2f}x shorter than serial), work {wk.sum() / ser.sum():.3f}x")
+
+
+if __name__ == "__main__":
+    main()
