@@ -98,7 +98,9 @@ def alg_bytes(cnt: dict, wb: dict, pixels: int) -> float:
             + cnt["env_lookups"] * wb["env_lookup"] + pixels * 12.0)
 
 
-def roofline(ctx, cnt: dict, kernel_ms: float, pixels: int, workload: str) -> dict:
+def roofline(ctx, cnt: dict, kernel_ms: float, pixels: int, workload: str, share: float = 1.0) -> dict:
+    """share: this launch's fraction of the frame (a rank's tile); the committed PMC summaries are
+    whole-frame launches and are scaled by it."""
     info = ctx.scene_info()
     brute = info["brute_records"] > 0
     prof = _profile(workload)
@@ -107,6 +109,8 @@ def roofline(ctx, cnt: dict, kernel_ms: float, pixels: int, workload: str) -> di
     byt = alg_bytes(cnt, ctx.work_bytes(), pixels)
     traffic = prof.get("hbm_bytes_per_launch")
     issued = prof.get("valu_lane_slots_per_launch")
+    traffic = traffic * share if traffic else traffic
+    issued = issued * share if issued else issued
     valu = {"achieved": round(ops / sec / 1e12, 3), "peak": VALU_PEAK_TOPS, "unit": "Tops/s",
             "frac": round(ops / sec / 1e12 / VALU_PEAK_TOPS, 4), "alg_ops_per_launch": int(ops),
             "issued": issued, "issued_frac": (round(issued / sec / 1e12 / VALU_PEAK_TOPS, 4) if issued else None)}
@@ -296,7 +300,7 @@ def main():
     # work counters of the same traversal on this rank's tile (instrumented launch, not timed)
     cnt = ctx.count_work_detail(cam, env, npix, spp, mb, rank, world)
     tile_pixels = D.tile_rows(npix, width, rank, world) * width
-    rf = roofline(ctx, cnt, kernel_ms, tile_pixels, wl.name)
+    rf = roofline(ctx, cnt, kernel_ms, tile_pixels, wl.name, share=tile_pixels / npix)
 
     frame_check = None
     if args.check and world > 1:
