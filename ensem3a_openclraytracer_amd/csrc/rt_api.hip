@@ -99,6 +99,7 @@ struct rt_ctx {
     int sun_any = 1;    // FAST tree walk: shadow rays end at their first hit when no material is glass
     int block = 128;
     int bvh_width = 0;  // FAST tree walk: 2 = BVH2 nodes, 4 = the 4-wide quantised layout, 0 = auto (option "bvh_width")
+    int fixed_point = 1;  // sum the repeats of a sample that draws no random number (FrameParams::fixed_point)
     std::string err;
 };
 
@@ -644,6 +645,7 @@ int check_frame(rt_ctx* ctx, const float* cam, const float* env, int64_t npix, i
     fp->sun_skip = (ctx->sun_skip && env[3] == 0.0f && env[4] >= 0.0f && ctx->hs.colors_finite) ? 1 : 0;
     fp->sun_any = (ctx->sun_any && !ctx->hs.has_glass) ? 1 : 0;
     fp->wide = use_wide(ctx) ? 1 : 0;
+    fp->fixed_point = ctx->fixed_point;
     fp->team = ctx->team;
     fp->max_waves = ctx->max_waves;
     fp->log_buf = nullptr;
@@ -781,6 +783,11 @@ int rt_set_option(rt_ctx* ctx, const char* key, int64_t value) {
     if (!std::strcmp(key, "waves")) {
         if (value < 0 || value > 8) return set_err(ctx, RT_ERR_ARG, "waves must be in 0..8");
         ctx->max_waves = (int)value;
+        return RT_OK;
+    }
+    if (!std::strcmp(key, "fixed_point")) {
+        if (value != 0 && value != 1) return set_err(ctx, RT_ERR_ARG, "fixed_point must be 0 or 1");
+        ctx->fixed_point = (int)value;
         return RT_OK;
     }
     if (!std::strcmp(key, "bvh_width")) {

@@ -101,6 +101,9 @@ struct FrameParams {
     // anything (Raytracing.cl:125-137), so its traversal ends at the first accepted triangle
     int32_t sun_any;
     int32_t wide;        // FAST tree walk over the 4-wide quantised layout (DevScene::wnodes)
+    // a sample that draws no random number (it ends at its first loop head: camera ray escaped or
+    // on an emitter) is every later sample of its pixel: the rest are summed without re-running it
+    int32_t fixed_point;
     // debug event log of one pixel (rt_debug_pixel_log only; unused by the product launches)
     int64_t log_pixel;
     float* log_buf;

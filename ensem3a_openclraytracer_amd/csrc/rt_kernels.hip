@@ -973,6 +973,14 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) r
                 acc = rtm_add(acc, so);
                 if (COUNT) c.samples++;
                 ++s;
+                // A sample that ends at its first loop head (j == 0: no bounce sampled) drew no random
+                // numbers, so the RNG state is unchanged and every later sample of the pixel is this
+                // sample again (same cached camera hit, same state): their colours are added in order,
+                // bit for bit the reference's sum (FrameParams::fixed_point).
+                if (TRAV == TRAV_FAST && F.fixed_point && j == 0 && !(LOG && logme)) {
+                    if (COUNT) c.samples += (unsigned long long)max(spp - s, 0);
+                    for (; s < spp; ++s) acc = rtm_add(acc, so);
+                }
                 if (s >= spp) {
                     phase = FETCH;
                 } else {
@@ -1389,6 +1397,7 @@ __global__ void __launch_bounds__(256) render_resume_kernel(DevScene S, FramePar
     rtm_f3 Bo = rtm_v3(0, 0, 0), Bd = rtm_v3(0, 0, 0);
     rtm_f3 acc = rtm_v3(0, 0, 0);
     int s = 0;
+    bool drew = false;   // the current sample has drawn random numbers (a diffuse or glossy bounce)
 
     auto write_pixel = [&]() __attribute__((always_inline)) {
         store_pixel(out, p, acc, spp);
@@ -1405,6 +1414,17 @@ __global__ void __launch_bounds__(256) render_resume_kernel(DevScene S, FramePar
         phase = s >= spp ? FETCH : PREP;
         Ro = C.position; Rd = cd; tri = tc; k = kc; j = 0;
         so = rtm_v3(1, 1, 1);
+        drew = false;
+    };
+    // A sample that drew no random numbers (camera ray escaped or on an emitter, or only glass
+    // bounces): the RNG state is unchanged, so every later sample of the pixel is this sample again.
+    // Their colours are added in order here (finish_sample adds the last), bit for bit the
+    // reference's sum (FrameParams::fixed_point).
+    auto repeat_fixed = [&]() __attribute__((always_inline)) {
+        if (F.fixed_point && !drew && !(LOG && logme)) {
+            if (COUNT) c.samples += (unsigned long long)max(spp - 1 - s, 0);
+            for (; s + 1 < spp; ++s) acc = rtm_add(acc, so);
+        }
     };
     auto start = [&](rtm_f3 o, rtm_f3 d) __attribute__((always_inline)) {
         tracing = !fast_init<COUNT>(S, T, o, d, c);
@@ -1453,6 +1473,7 @@ __global__ void __launch_bounds__(256) render_resume_kernel(DevScene S, FramePar
                 kc = h.k;
                 Ro = C.position; Rd = cd; tri = tc; k = kc; j = 0;
                 so = rtm_v3(1, 1, 1);
+                drew = false;
                 phase = PREP;
                 if (spp <= 0) {   // reference: output = 0/0 -> NaN -> clamp gives 1
                     write_pixel();
@@ -1469,6 +1490,7 @@ __global__ void __launch_bounds__(256) render_resume_kernel(DevScene S, FramePar
                     if (bm.type != 0) {
                         if (j == maxB) {
                             so = rtm_v3(0, 0, 0);
+                            repeat_fixed();
                             finish_sample();
                         } else {
                             ++j;
@@ -1476,6 +1498,7 @@ __global__ void __launch_bounds__(256) render_resume_kernel(DevScene S, FramePar
                         }
                     } else {
                         so = rtm_scale(so, bm.rough);
+                        repeat_fixed();
                         finish_sample();
                     }
                 } else {
@@ -1504,14 +1527,17 @@ __global__ void __launch_bounds__(256) render_resume_kernel(DevScene S, FramePar
                 }
                 const rtm_f3 envLight = rtm_scale(sample_ibl_if<COUNT>(S, C, Bd, e4, c), e4);
                 so = rtm_mul(so, rtm_add(sunLight, envLight));
+                repeat_fixed();
                 finish_sample();
             }
             // naiveGI loop heads (Raytracing.cl:46-79) until a ray is needed or the pixel is done
             while (phase == PREP) {
                 if (j > maxB) {
+                    repeat_fixed();
                     finish_sample();   // naiveGI's loop never entered (maxBounce < 0): the sample stays 1
                 } else if (tri < 0) {
                     so = rtm_scale(rtm_mul(so, sample_ibl_if<COUNT>(S, C, Rd, e4, c)), e4);
+                    repeat_fixed();
                     finish_sample();
                 } else {
                     const float4 sh = S.tri_shade[tri];
@@ -1519,6 +1545,7 @@ __global__ void __launch_bounds__(256) render_resume_kernel(DevScene S, FramePar
                     const Mat cm = load_mat(S.mat, __float_as_int(sh.w));
                     if (cm.type == 0) {
                         so = rtm_scale(so, cm.rough);
+                        repeat_fixed();
                         finish_sample();
                     } else {
                         const float4 f2 = S.tri_frame[3 * tri + 2];
@@ -1526,6 +1553,7 @@ __global__ void __launch_bounds__(256) render_resume_kernel(DevScene S, FramePar
                         float invPdf = 0.0f;
                         rtm_f3 brdf = rtm_v3(0, 0, 0);
                         if (COUNT) count_event(c, cm.type);
+                        drew = drew || cm.type != 3;
                         if (cm.type == 1) {
                             Bd = hemi_cosine(n, S.tri_frame[3 * tri], S.tri_frame[3 * tri + 1], f2, &seed1, &seed0,
                                              &invPdf);

@@ -81,10 +81,12 @@ def test_work_counters_match_oracle(kl, traversal):
     _launch(kl, sc, cam, env, npix, spp, mb, ibl, traversal)
     _, oc = O.render(O.OracleScene.from_scene(sc, ibl), cam, env, npix, spp, mb, nthreads=16, counts=True)
     kl.native.set_option("sun_skip", 0)   # count every ray the reference traces (this case's sun is unlit)
+    kl.native.set_option("fixed_point", 0)   # ... and every repeat of a sample that draws nothing
     try:
         gc = kl.native.count_work(cam, env, npix, spp, mb)
     finally:
         kl.native.set_option("sun_skip", 1)
+        kl.native.set_option("fixed_point", 1)
     assert gc["rays"] == oc["rays"] and gc["env_lookups"] == oc["env"]
     if traversal == "ref":
         assert gc["node_fetches"] == oc["nodes"] and gc["tri_tests"] == oc["tris"]
@@ -665,3 +667,32 @@ def test_wide_layout_renders_identically(kl, case):
     with pytest.raises(_native.NativeError, match="bvh_width"):
         kl.native.set_option("bvh_width", 8)
 
+
+
+@pytest.mark.parametrize("case", ["serre_96x54_s4", "cornell_128_s16", "monkey_c3_64_s4", "serre_sky_s64"])
+def test_fixed_point_samples_render_identically(kl, case):
+    """fixed_point: a sample that ends at its first loop head (camera ray escaped to the IBL, or on an
+    emitter) draws no random number, so every later sample of the pixel repeats it; their colours are
+    summed in order without re-running them.  Same frame as re-running every sample and as the
+    oracle, on the brute-force path (cornell) and the tree walk (serre: 3/4 of its pixels are sky),
+    and the work counters still report every sample."""
+    if case == "serre_sky_s64":
+        sc, cam, env, npix, spp, mb, ibl = W.PARITY_CASES["serre_96x54_s4"].inputs()
+        spp = 64
+    else:
+        sc, cam, env, npix, spp, mb, ibl = W.PARITY_CASES[case].inputs()
+    try:
+        kl.native.set_option("fixed_point", 0)
+        full = _launch(kl, sc, cam, env, npix, spp, mb, ibl, "fast")
+        c0 = kl.native.count_work_detail(cam, env, npix, spp, mb)
+        kl.native.set_option("fixed_point", 1)
+        fast = _launch(kl, sc, cam, env, npix, spp, mb, ibl, "fast")
+        c1 = kl.native.count_work_detail(cam, env, npix, spp, mb)
+    finally:
+        kl.native.set_option("fixed_point", 1)
+    np.testing.assert_array_equal(fast, full)
+    np.testing.assert_array_equal(fast, _oracle(sc, cam, env, npix, spp, mb, ibl))
+    assert c1["samples"] == c0["samples"] == npix * spp
+    assert c1["rays"] <= c0["rays"]
+    with pytest.raises(_native.NativeError, match="fixed_point"):
+        kl.native.set_option("fixed_point", 2)
