@@ -663,6 +663,43 @@ __device__ __forceinline__ rtm_f3 hemi_uniform(rtm_f3 n, float4 f0, float4 f1, f
     return w;
 }
 
+// hemi_cosine (cosine = true) and hemi_uniform in one instruction stream: a wave that shades
+// diffuse and glossy bounces together runs the two draws, one sincos and the rotation once instead
+// of once per branch.  Per lane the operations are those of the two samplers above, so the same bits:
+// both first angles are 6.28 times one draw (cosine: theta = rb * 2 * 3.14, uniform: phi = 2 * 3.14 *
+// ra) and localV.xy = A * (cos, sin) of it with A = sqrt(u) or sin(theta) (products commute exactly).
+__device__ __forceinline__ rtm_f3 hemi_sample(bool cosine, rtm_f3 n, float4 f0, float4 f1, float4 f2, uint32_t* s0,
+                                              uint32_t* s1, float* invPdf) {
+    const float ra = rtm_rand(s0, s1);
+    const float rb = rtm_rand(s0, s1);
+    const float ang = cosine ? rb * 2.0f * 3.14f : 2.0f * 3.14f * ra;
+    float sa, ca;
+    rtm_sincos(ang, &sa, &ca);
+    float A, Z;
+    if (cosine) {
+        A = sqrtf(ra);
+        Z = sqrtf(rtm_fmax(0.0f, 1.0f - ra));
+    } else {
+        float sth, cth;
+        rtm_sincos(rtm_acos(1.0f - rb), &sth, &cth);
+        A = sth;
+        Z = cth;
+    }
+    const rtm_f3 localV = rtm_v3(A * ca, A * sa, Z);
+    rtm_f3 l;
+    if (f2.w != 0.0f) {
+        l = rtm_scale(localV, n.z);
+    } else {
+        rtm_rot R;
+        R.q = rtm_v4(f0.x, f0.y, f0.z, f0.w);
+        R.qinv = rtm_v4(f1.x, f1.y, f1.z, f1.w);
+        l = rtm_rot_apply(R, localV);
+        if (cosine) l = rtm_normalize(l);
+    }
+    *invPdf = cosine ? 3.14f / (rtm_fmax(rtm_dot(l, n), 0.0f)) : 2.0f * 3.14f;
+    return l;
+}
+
 // ---- BRDF_GGX, MathLib.cl:461-500 ----
 __device__ __forceinline__ rtm_f3 brdf_ggx(rtm_f3 color, float rough, rtm_f3 v, rtm_f3 l, rtm_f3 n) {
     const rtm_f3 h = rtm_normalize(rtm_add(l, v));
@@ -1554,14 +1591,11 @@ __global__ void __launch_bounds__(256) render_resume_kernel(DevScene S, FramePar
                         rtm_f3 brdf = rtm_v3(0, 0, 0);
                         if (COUNT) count_event(c, cm.type);
                         drew = drew || cm.type != 3;
-                        if (cm.type == 1) {
-                            Bd = hemi_cosine(n, S.tri_frame[3 * tri], S.tri_frame[3 * tri + 1], f2, &seed1, &seed0,
-                                             &invPdf);
-                            brdf = rtm_scale(cm.color, 1.0f / 3.14f);
-                        } else if (cm.type == 2) {
-                            Bd = hemi_uniform(n, S.tri_frame[3 * tri], S.tri_frame[3 * tri + 1], f2, &seed1, &seed0,
-                                              &invPdf);
-                            brdf = brdf_ggx(cm.color, cm.rough, rtm_scale(Rd, -1.0f), Bd, n);
+                        if (cm.type != 3) {   // diffuse (1) or glossy (2): one sampler stream for both
+                            Bd = hemi_sample(cm.type == 1, n, S.tri_frame[3 * tri], S.tri_frame[3 * tri + 1], f2,
+                                             &seed1, &seed0, &invPdf);
+                            if (cm.type == 1) brdf = rtm_scale(cm.color, 1.0f / 3.14f);
+                            else brdf = brdf_ggx(cm.color, cm.rough, rtm_scale(Rd, -1.0f), Bd, n);
                         } else {
                             Bd = Rd;
                             brdf = cm.color;
