@@ -7,7 +7,8 @@
 One "step" = one full frame of the configuration (default C2: Cornell box
 1024x1024, 64 spp, maxBounce 4): every rank renders its row-interleaved tile with
 the HIP kernel (scene and IBL already resident in HBM), rank 0 gathers the tiles
-over RCCL and assembles the frame.  K steps are timed between barrier +
+over RCCL and assembles the frame (frame k's gather overlaps frame k+1's render:
+two tile buffers; the timed region ends after the last frame is assembled).  K steps are timed between barrier +
 synchronize fences; the max over ranks is reported.  value = W*H*spp / time in
 Msamples/s (whole job; the frame size is fixed, so scaling is "strong").
 
@@ -260,32 +261,52 @@ def main():
     width = int(cam[6])
     stream = torch.cuda.current_stream()
     mrows = D.max_tile_rows(npix, width, world)
-    tile = torch.zeros(3 * width * mrows, dtype=torch.float32, device="cuda")
-    bufs = [torch.empty(tile.numel(), dtype=torch.float32, device=coll) for _ in range(world)] \
-        if (world > 1 and rank == 0) else None
+    # N > 1: two tile buffers, so that frame k's RCCL gather (on the collective's own stream) overlaps
+    # frame k+1's render; rank 0 assembles frame k once its gather is done
+    nbuf = 2 if world > 1 else 1
+    tiles = [torch.zeros(3 * width * mrows, dtype=torch.float32, device="cuda") for _ in range(nbuf)]
+    tile = tiles[0]
+    bufs = [[torch.empty(tile.numel(), dtype=torch.float32, device=coll) for _ in range(world)] for _ in range(nbuf)] \
+        if (world > 1 and rank == 0) else [None] * nbuf
     frame = torch.empty(3 * npix, dtype=torch.float32, device=coll) if (rank == 0 and world > 1) else None
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    pending = []   # (work, buffer index) of the gather in flight
 
-    def step(i=None):
+    def finish_pending():
+        while pending:
+            work, b = pending.pop(0)
+            if work is not None:
+                work.wait()   # the current stream waits for the gather (no host block for RCCL)
+            if rank == 0:
+                D.assemble(bufs[b], width, npix, world, out=frame)
+
+    def step(i=None, k=0):
+        b = k % nbuf
         if i is not None:
             ev[i][0].record(stream)
-        ctx.render_device(cam, env, npix, spp, mb, rank, world, tile.data_ptr(), stream.cuda_stream)
+        ctx.render_device(cam, env, npix, spp, mb, rank, world, tiles[b].data_ptr(), stream.cuda_stream)
         if i is not None:
             ev[i][1].record(stream)
         if world > 1:
-            dist.gather(tile if coll == "cuda" else tile.cpu(), gather_list=bufs, dst=0)
-            if rank == 0:
-                D.assemble(bufs, width, npix, world, out=frame)
+            if coll == "cuda":
+                work = dist.gather(tiles[b], gather_list=bufs[b], dst=0, async_op=True)
+            else:   # one-GPU gloo rehearsal: host copies, synchronous
+                dist.gather(tiles[b].cpu(), gather_list=bufs[b], dst=0)
+                work = None
+            finish_pending()      # the previous frame's gather ran while this frame rendered
+            pending.append((work, b))
 
-    for _ in range(args.warmup):
-        step()
+    for w in range(args.warmup):
+        step(k=w)
+    finish_pending()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(args.steps):
-        step(i)
+        step(i, k=i)
+    finish_pending()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -305,6 +326,7 @@ def main():
     frame_check = None
     if args.check and world > 1:
         step()
+        finish_pending()
         torch.cuda.synchronize()
         if rank == 0:
             full = torch.empty(3 * npix, dtype=torch.float32, device="cuda")
