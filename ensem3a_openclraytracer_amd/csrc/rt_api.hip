@@ -47,6 +47,7 @@ struct Device {
     int cus = 0;                  // compute units (sizes the FAST stack overflow buffer)
     DevBuf stack_ovf;             // FAST traversal stack entries beyond the LDS part
     DevBuf nodes, wnodes, wleaves, tri_fast, brute, brute_box, bvh9, tri_geo, tri_shade, tri_frame, mat, ibl, out, out8, counts, work, scratch_a, scratch_b;
+    DevBuf pilot;                 // two-pass launches: per-pixel state, cost and order (FrameParams::pilot_*)
     char* host_stage = nullptr;   // pinned staging for rt_render / rt_render_rgb8
     size_t host_stage_bytes = 0;
     // Every launch of this context on the device shares `work` (pixel counters + launch constants)
@@ -100,6 +101,7 @@ struct rt_ctx {
     int block = 128;
     int bvh_width = 0;  // FAST tree walk: 2 = BVH2 nodes, 4 = the 4-wide quantised layout, 0 = auto (option "bvh_width")
     int fixed_point = 1;  // sum the repeats of a sample that draws no random number (FrameParams::fixed_point)
+    int pilot = -1;       // two-pass launches: pilot samples per pixel (0 = one pass, -1 = auto; FrameParams::pilot)
     std::string err;
 };
 
@@ -646,6 +648,11 @@ int check_frame(rt_ctx* ctx, const float* cam, const float* env, int64_t npix, i
     fp->sun_any = (ctx->sun_any && !ctx->hs.has_glass) ? 1 : 0;
     fp->wide = use_wide(ctx) ? 1 : 0;
     fp->fixed_point = ctx->fixed_point;
+    fp->pass = 0;
+    fp->pilot = 0;
+    fp->pilot_state = nullptr;
+    fp->pilot_cost = nullptr;
+    fp->pilot_order = nullptr;
     fp->team = ctx->team;
     fp->max_waves = ctx->max_waves;
     fp->log_buf = nullptr;
@@ -706,7 +713,7 @@ void rt_destroy(rt_ctx* ctx) {
         if (d.pending) (void)hipEventSynchronize(d.done);
         if (d.stream) (void)hipStreamSynchronize(d.stream);
         for (DevBuf* b : {&d.stack_ovf, &d.nodes, &d.wnodes, &d.wleaves, &d.tri_fast, &d.brute, &d.brute_box, &d.bvh9, &d.tri_geo, &d.tri_shade, &d.tri_frame, &d.mat, &d.ibl, &d.out,
-                          &d.counts, &d.work, &d.scratch_a, &d.scratch_b})
+                          &d.out8, &d.counts, &d.work, &d.scratch_a, &d.scratch_b, &d.pilot})
             release(*b);
         if (d.host_stage) (void)hipHostFree(d.host_stage);
         if (d.stream) (void)hipStreamDestroy(d.stream);
@@ -783,6 +790,11 @@ int rt_set_option(rt_ctx* ctx, const char* key, int64_t value) {
     if (!std::strcmp(key, "waves")) {
         if (value < 0 || value > 8) return set_err(ctx, RT_ERR_ARG, "waves must be in 0..8");
         ctx->max_waves = (int)value;
+        return RT_OK;
+    }
+    if (!std::strcmp(key, "pilot")) {
+        if (value < -1 || value > (1 << 20)) return set_err(ctx, RT_ERR_ARG, "pilot must be -1 (auto), 0 (off) or a sample count");
+        ctx->pilot = (int)value;
         return RT_OK;
     }
     if (!std::strcmp(key, "fixed_point")) {
@@ -942,6 +954,34 @@ int64_t rt_tile_rows(int64_t npix, int width, int row0, int row_step) {
     return (H - row0 + row_step - 1) / row_step;
 }
 
+namespace {
+// Two-pass launches (FrameParams::pass): FAST tree-walk renders of tiles with more pixels than the
+// device keeps lanes resident get a pilot pass of spp / 8 samples (option "pilot": -1 auto, 0 off,
+// or K), whose per-pixel costs order the rest of the frame, most expensive first (rt_kernels.hip
+// launch_render).  Sets fp's pilot fields and sizes the device's scratch for them.
+hipError_t setup_pilot(rt_ctx* ctx, Device& d, rt::FrameParams& fp) {
+    if (ctx->pilot == 0 || effective_traversal(ctx) != RT_TRAVERSAL_FAST || fp.nloc <= 0) return hipSuccess;
+    int k = ctx->pilot;
+    if (k < 0) {   // auto: the tree walk on tiles of 1-16 pixels per resident lane (where the tail is long)
+        const int64_t lanes = (int64_t)std::max(d.cus, 1) * 1280;
+        if (ctx->hs.nbrute > 0 || fp.spp < 16 || fp.nloc <= lanes || fp.nloc > 16 * lanes) return hipSuccess;
+        k = fp.spp / 8;
+    }
+    if (k >= fp.spp) return hipSuccess;
+    const size_t n = (size_t)fp.nloc;
+    // state 32 B | cost 4 B | order 4 B per pixel, cost histogram + offsets (2 x 256), and the chunk
+    // costs + chunk order (at most one chunk per pixel: the tree walk orders single pixels)
+    hipError_t e = ensure(d.pilot, n * 32 + n * 8 + 2 * 256 * sizeof(uint32_t) + 2 * (n + 1) * sizeof(uint32_t));
+    if (e != hipSuccess) return e;
+    char* base = (char*)d.pilot.p;
+    fp.pilot = k;
+    fp.pilot_state = (float4*)base;
+    fp.pilot_cost = (uint32_t*)(base + n * 32);
+    fp.pilot_order = (const uint32_t*)(base + n * 36);
+    return hipSuccess;
+}
+}  // namespace
+
 int rt_render_device(rt_ctx* ctx, int device_index, const float cam[10], const float env[5], int64_t npix, int spp,
                      int max_bounce, int row0, int row_step, float* d_out, void* stream) {
     rt::FrameParams fp;
@@ -956,6 +996,7 @@ int rt_render_device(rt_ctx* ctx, int device_index, const float cam[10], const f
     HIP_OR_RET(ctx, hipSetDevice(d.id));
     hipStream_t s = (hipStream_t)stream;  // NULL = the device's default (null) stream, HIP convention
     HIP_OR_RET(ctx, order_after_last(d, s));
+    HIP_OR_RET(ctx, setup_pilot(ctx, d, fp));
     HIP_OR_RET(ctx, rt::launch_render(dev_scene(ctx, d), fp, effective_traversal(ctx), ctx->block, d_out, nullptr,
                                       (unsigned int*)d.work.p, s));
     HIP_OR_RET(ctx, mark_launch(d, s));
@@ -996,6 +1037,7 @@ int render_host(rt_ctx* ctx, const float cam[10], const float env[5], int64_t np
             d.host_stage_bytes = bytes;
         }
         HIP_OR_RET(ctx, order_after_last(d, d.stream));
+        HIP_OR_RET(ctx, setup_pilot(ctx, d, fp));
         HIP_OR_RET(ctx, rt::launch_render(dev_scene(ctx, d), fp, effective_traversal(ctx), ctx->block,
                                           (float*)d.out.p, nullptr, (unsigned int*)d.work.p, d.stream));
         HIP_OR_RET(ctx, mark_launch(d, d.stream));

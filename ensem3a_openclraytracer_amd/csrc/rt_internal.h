@@ -104,6 +104,16 @@ struct FrameParams {
     // a sample that draws no random number (it ends at its first loop head: camera ray escaped or
     // on an emitter) is every later sample of its pixel: the rest are summed without re-running it
     int32_t fixed_point;
+    // Two-pass launches (launch_render, option "pilot"): pass 1 renders the first `pilot` samples of
+    // every pixel and saves each unfinished pixel's state (pilot_state: acc.xyz | kc, seed0 seed1 tc s)
+    // and the rays it traced (pilot_cost); the pixels are then ordered by that cost, most first
+    // (pilot_order); pass 2 continues them in that order, so the last pixels a frame starts are the
+    // short ones.  pass 0 = one pass.
+    int32_t pass;
+    int32_t pilot;
+    float4* pilot_state;
+    uint32_t* pilot_cost;
+    const uint32_t* pilot_order;
     // debug event log of one pixel (rt_debug_pixel_log only; unused by the product launches)
     int64_t log_pixel;
     float* log_buf;

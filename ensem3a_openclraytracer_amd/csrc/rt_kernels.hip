@@ -930,6 +930,16 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) r
     rtm_f3 Bo = rtm_v3(0, 0, 0), Bd = rtm_v3(0, 0, 0);
     rtm_f3 acc = rtm_v3(0, 0, 0);
     int s = 0;
+    int cost = 0;   // pass 1: rays this pixel traced (pilot_cost)
+
+    // pass 1 (FrameParams::pass): after the pilot samples, save the pixel's state for pass 2; the
+    // pixel is written (and its cost set to 0) when all its samples are done
+    auto save_pilot = [&]() __attribute__((always_inline)) {
+        F.pilot_state[2 * (int64_t)p] = make_float4(acc.x, acc.y, acc.z, kc);
+        F.pilot_state[2 * (int64_t)p + 1] =
+            make_float4(__uint_as_float(seed0), __uint_as_float(seed1), __int_as_float(tc), __int_as_float(s));
+        F.pilot_cost[p] = s >= spp ? 0u : (unsigned)cost;
+    };
 
     while (true) {
         // -- refill: ballot the lanes that need a pixel, one atomic per wave --
@@ -940,7 +950,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) r
             if (phase == FETCH) {
                 bool ok = q < nloc;
                 if (ok) {
-                    p = (int)q;
+                    p = F.pass == 2 ? (int)F.pilot_order[q] : (int)q;
                     const int krow = p / W;
                     const int col = p - krow * W;
                     const int64_t i64 = ((int64_t)F.row0 + (int64_t)krow * F.row_step) * W + col;
@@ -953,16 +963,30 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) r
                     cd = camera_dir(C, W, i);
                     acc = rtm_v3(0, 0, 0);
                     s = 0;
+                    cost = 0;
                     phase = PRIMARY;
                     logme = LOG && i == F.log_pixel;
+                    if (F.pass == 2) {   // continue from the pilot state: camera hit cached, sample s next
+                        const float4 a = F.pilot_state[2 * (int64_t)p], b = F.pilot_state[2 * (int64_t)p + 1];
+                        acc = rtm_v3(a.x, a.y, a.z);
+                        kc = a.w;
+                        seed0 = __float_as_uint(b.x);
+                        seed1 = __float_as_uint(b.y);
+                        tc = __float_as_int(b.z);
+                        s = __float_as_int(b.w);
+                        Ro = C.position; Rd = cd; tri = tc; k = kc; j = 0;
+                        so = rtm_v3(1, 1, 1);
+                        phase = s >= spp ? FETCH : PREP;   // finished in pass 1: already written
+                    }
                 } else {
-                    phase = DONE;
+                    // past the tile, or (pass 2, pixels in cost order) a padding pixel past the frame
+                    phase = (F.pass == 2 && q < nloc) ? FETCH : DONE;
                 }
             }
         }
         if (__all(phase == DONE)) break;
         if (COUNT && lane == 0) c.wave_outer++;
-        if (phase == DONE) continue;
+        if (phase == DONE || phase == FETCH) continue;   // FETCH: a pass-2 pixel finished in pass 1
 
         if (phase == PREP) {
             // naiveGI loop head for bounce j (Raytracing.cl:46-79); may complete samples without tracing
@@ -1020,12 +1044,14 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) r
                 }
                 if (s >= spp) {
                     phase = FETCH;
+                    if (team_leader) store_pixel(out, p, acc, spp);
+                    if (F.pass == 1) save_pilot();
+                } else if (F.pass == 1 && s >= F.pilot) {
+                    save_pilot();
+                    phase = FETCH;
                 } else {
                     Ro = C.position; Rd = cd; tri = tc; k = kc; j = 0;
                     so = rtm_v3(1, 1, 1);
-                }
-                if (phase == FETCH) {
-                    if (team_leader) store_pixel(out, p, acc, spp);
                 }
                 continue;
             }
@@ -1035,6 +1061,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) r
         const rtm_f3 to = (phase == PRIMARY) ? C.position : Bo;
         const rtm_f3 td = (phase == PRIMARY) ? cd : ((phase == BOUNCE) ? Bd : C.sun);
         const Hit h = trace<TRAV, COUNT, SMEM, OVF, BRUTE != 0>(S, nodes, tris, to, td, stk, B, lst, c, mtrec, ts, boxrec);
+        ++cost;
         bool finish = false;
         if (phase == PRIMARY) {
             tc = h.tri;
@@ -1097,6 +1124,10 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) r
             ++s;
             if (s >= spp) {
                 if (team_leader) store_pixel(out, p, acc, spp);
+                if (F.pass == 1) save_pilot();
+                phase = FETCH;
+            } else if (F.pass == 1 && s >= F.pilot) {
+                save_pilot();
                 phase = FETCH;
             } else {
                 Ro = C.position; Rd = cd; tri = tc; k = kc; j = 0;
@@ -1435,9 +1466,18 @@ __global__ void __launch_bounds__(256) render_resume_kernel(DevScene S, FramePar
     rtm_f3 acc = rtm_v3(0, 0, 0);
     int s = 0;
     bool drew = false;   // the current sample has drawn random numbers (a diffuse or glossy bounce)
+    int cost = 0;        // pass 1: rays this pixel traced (pilot_cost)
 
     auto write_pixel = [&]() __attribute__((always_inline)) {
         store_pixel(out, p, acc, spp);
+    };
+    // pass 1 (FrameParams::pass): after the pilot samples, save the pixel's state for pass 2; the
+    // pixel is written (and its cost set to 0) when all its samples are done
+    auto save_pilot = [&]() __attribute__((always_inline)) {
+        F.pilot_state[2 * (int64_t)p] = make_float4(acc.x, acc.y, acc.z, kc);
+        F.pilot_state[2 * (int64_t)p + 1] =
+            make_float4(__uint_as_float(seed0), __uint_as_float(seed1), __int_as_float(tc), __int_as_float(s));
+        F.pilot_cost[p] = s >= spp ? 0u : (unsigned)cost;
     };
     auto finish_sample = [&]() __attribute__((always_inline)) {  // output += baseColor; next sample from the cached camera hit
         if (LOG && logme) log_event(F, 3.0f, s + 1, rtm_v3(0, 0, 0), rtm_v3(0, 0, 0), 0.0f, 0, so);
@@ -1445,10 +1485,12 @@ __global__ void __launch_bounds__(256) render_resume_kernel(DevScene S, FramePar
         if (COUNT) c.samples++;
         ++s;
         if (s >= spp) write_pixel();
+        const bool stop = F.pass == 1 && (s >= spp || s >= F.pilot);
+        if (stop) save_pilot();
         // the next sample restarts from the cached camera hit; written as selects so that no branch
         // ends in a store the compiler could merge with the pixel store (that would force the path
         // state into scratch memory through a generic pointer)
-        phase = s >= spp ? FETCH : PREP;
+        phase = (s >= spp || stop) ? FETCH : PREP;
         Ro = C.position; Rd = cd; tri = tc; k = kc; j = 0;
         so = rtm_v3(1, 1, 1);
         drew = false;
@@ -1464,6 +1506,7 @@ __global__ void __launch_bounds__(256) render_resume_kernel(DevScene S, FramePar
         }
     };
     auto start = [&](rtm_f3 o, rtm_f3 d) __attribute__((always_inline)) {
+        ++cost;
         tracing = !fast_init<COUNT>(S, T, o, d, c);
         if (WIDE) T.item = S.wroot_ref;
         T.any = false;
@@ -1478,7 +1521,7 @@ __global__ void __launch_bounds__(256) render_resume_kernel(DevScene S, FramePar
             if (phase == FETCH) {
                 bool ok = q < nloc;
                 if (ok) {
-                    p = (int)q;
+                    p = F.pass == 2 ? (int)F.pilot_order[q] : (int)q;
                     const int krow = p / W;
                     const int col = p - krow * W;
                     const int64_t i64 = ((int64_t)F.row0 + (int64_t)krow * F.row_step) * W + col;
@@ -1491,11 +1534,27 @@ __global__ void __launch_bounds__(256) render_resume_kernel(DevScene S, FramePar
                     cd = camera_dir(C, W, i);
                     acc = rtm_v3(0, 0, 0);
                     s = 0;
+                    cost = 0;
                     phase = PRIMARY;
                     logme = LOG && i == F.log_pixel;
-                    start(C.position, cd);
+                    if (F.pass == 2) {   // continue from the pilot state: camera hit cached, sample s next
+                        const float4 a = F.pilot_state[2 * (int64_t)p], b = F.pilot_state[2 * (int64_t)p + 1];
+                        acc = rtm_v3(a.x, a.y, a.z);
+                        kc = a.w;
+                        seed0 = __float_as_uint(b.x);
+                        seed1 = __float_as_uint(b.y);
+                        tc = __float_as_int(b.z);
+                        s = __float_as_int(b.w);
+                        Ro = C.position; Rd = cd; tri = tc; k = kc; j = 0;
+                        so = rtm_v3(1, 1, 1);
+                        drew = false;
+                        phase = s >= spp ? FETCH : PREP;   // finished in pass 1: already written
+                    } else {
+                        start(C.position, cd);
+                    }
                 } else {
-                    phase = DONE;
+                    // past the tile, or (pass 2, pixels in cost order) a padding pixel past the frame
+                    phase = (F.pass == 2 && q < nloc) ? FETCH : DONE;
                 }
             }
         }
@@ -1872,7 +1931,106 @@ hipError_t launch_fast(const DevScene& sc, const FrameParams& fp, int block, flo
     return launch_t<TRAV_FAST, COUNT, false>(sc, fp, block, d_out, d_counts, d_work, stream);
 }
 
+// ---- two-pass ordering (FrameParams::pass): pilot costs -> pixel order, most expensive first ----
+// Pixels are ordered in chunks of `chunk` consecutive tile pixels: the chunks by their summed pilot
+// cost, the pixels of a chunk in tile order.  The tree walk orders single pixels (its lanes diverge
+// anyway); the brute-force path would need chunks of a wave (64) to keep neighbouring lanes on
+// neighbouring pixels -- its box loop and shading branches pay per wave -- and then gains nothing,
+// so it runs one pass unless asked.
+constexpr int kCostBins = 256;
+
+__global__ void pilot_chunk_kernel(const uint32_t* __restrict__ cost, int64_t nfull, int chunk,
+                                   uint32_t* __restrict__ ccost) {
+    for (int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; c < nfull; c += (int64_t)gridDim.x * blockDim.x) {
+        uint32_t t = 0;
+        for (int k = 0; k < chunk; ++k) t += cost[c * chunk + k];
+        ccost[c] = t;
+    }
+}
+
+__device__ __forceinline__ uint32_t cost_bin(uint32_t v, uint32_t scale) {
+    return min((uint32_t)(kCostBins - 1), (uint32_t)(((uint64_t)v * scale) >> 16));
+}
+
+__global__ void pilot_hist_kernel(const uint32_t* __restrict__ ccost, int64_t n, uint32_t scale,
+                                  uint32_t* __restrict__ hist) {
+    __shared__ uint32_t h[kCostBins];
+    for (int b = threadIdx.x; b < kCostBins; b += blockDim.x) h[b] = 0;
+    __syncthreads();
+    for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < n; q += (int64_t)gridDim.x * blockDim.x)
+        atomicAdd(&h[cost_bin(ccost[q], scale)], 1u);
+    __syncthreads();
+    for (int b = threadIdx.x; b < kCostBins; b += blockDim.x)
+        if (h[b]) atomicAdd(&hist[b], h[b]);
+}
+
+// offs[b] = number of chunks in bins above b (descending cost order); one block of kCostBins threads
+__global__ void pilot_scan_kernel(const uint32_t* __restrict__ hist, uint32_t* __restrict__ offs) {
+    __shared__ uint32_t t[kCostBins];
+    const int b = threadIdx.x;
+    t[b] = hist[b];
+    __syncthreads();
+    uint32_t above = 0;
+    for (int c = b + 1; c < kCostBins; ++c) above += t[c];
+    offs[b] = above;
+}
+
+__global__ void pilot_scatter_kernel(const uint32_t* __restrict__ ccost, int64_t n, uint32_t scale,
+                                     uint32_t* __restrict__ offs, uint32_t* __restrict__ corder) {
+    for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < n; q += (int64_t)gridDim.x * blockDim.x)
+        corder[atomicAdd(&offs[cost_bin(ccost[q], scale)], 1u)] = (uint32_t)q;
+}
+
+// pixel order: the full chunks in cost order, then the last partial chunk (if any) in place
+__global__ void pilot_expand_kernel(const uint32_t* __restrict__ corder, int64_t nfull, int chunk, int64_t nloc,
+                                    uint32_t* __restrict__ order) {
+    for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < nloc; q += (int64_t)gridDim.x * blockDim.x)
+        order[q] = q < nfull * chunk ? corder[q / chunk] * (uint32_t)chunk + (uint32_t)(q % chunk) : (uint32_t)q;
+}
+
+hipError_t launch_render_pass(const DevScene& sc, const FrameParams& fp, int traversal, int block, float* d_out,
+                              unsigned long long* d_counts, unsigned int* d_work, hipStream_t stream);
+
+// Two passes (fp.pilot > 0, product launches only): the first fp.pilot samples of every pixel,
+// then the rest of each pixel in descending order of the rays its (chunk's) pilot samples traced.  The
+// frame ends when its last-started pixels finish; started last, the cheapest pixels make that tail
+// short.  Every pixel's samples run in the same order as in one pass, so the frame is bit-identical.
 hipError_t launch_render(const DevScene& sc, const FrameParams& fp, int traversal, int block, float* d_out,
+                         unsigned long long* d_counts, unsigned int* d_work, hipStream_t stream) {
+    if (fp.pilot <= 0 || fp.pass != 0 || d_counts || fp.spp <= fp.pilot || fp.nloc <= 0 || !fp.pilot_state)
+        return launch_render_pass(sc, fp, traversal, block, d_out, d_counts, d_work, stream);
+    FrameParams a = fp;
+    a.pass = 1;
+    hipError_t e = launch_render_pass(sc, a, traversal, block, d_out, nullptr, d_work, stream);
+    if (e != hipSuccess) return e;
+    // scratch after the pixel order (rt_api.hip setup_pilot): hist | offs | chunk costs | chunk order
+    uint32_t* order = const_cast<uint32_t*>(fp.pilot_order);
+    uint32_t* hist = order + fp.nloc;
+    uint32_t* offs = hist + kCostBins;
+    const int chunk = sc.nbrute > 0 ? 64 : 1;
+    const int64_t nfull = fp.nloc / chunk;
+    uint32_t* ccost = offs + kCostBins;
+    uint32_t* corder = ccost + nfull;
+    // cost bins over a chunk's rays up to 2 (maxBounce + 1) rays per pilot sample per pixel
+    const uint64_t top = (uint64_t)chunk * fp.pilot * 2u * (uint64_t)(std::max(fp.max_bounce, 0) + 1);
+    const uint32_t scale = (uint32_t)std::max<uint64_t>(1, ((uint64_t)kCostBins << 16) / std::max<uint64_t>(top, 1));
+    e = hipMemsetAsync(hist, 0, kCostBins * sizeof(uint32_t), stream);
+    if (e != hipSuccess) return e;
+    const unsigned gc = (unsigned)std::max<int64_t>(1, std::min<int64_t>((nfull + 255) / 256, 2048));
+    const unsigned gp = (unsigned)std::min<int64_t>((fp.nloc + 255) / 256, 2048);
+    if (nfull > 0) {
+        hipLaunchKernelGGL(pilot_chunk_kernel, dim3(gc), dim3(256), 0, stream, fp.pilot_cost, nfull, chunk, ccost);
+        hipLaunchKernelGGL(pilot_hist_kernel, dim3(gc), dim3(256), 0, stream, ccost, nfull, scale, hist);
+        hipLaunchKernelGGL(pilot_scan_kernel, dim3(1), dim3(kCostBins), 0, stream, hist, offs);
+        hipLaunchKernelGGL(pilot_scatter_kernel, dim3(gc), dim3(256), 0, stream, ccost, nfull, scale, offs, corder);
+    }
+    hipLaunchKernelGGL(pilot_expand_kernel, dim3(gp), dim3(256), 0, stream, corder, nfull, chunk, fp.nloc, order);
+    FrameParams b = fp;
+    b.pass = 2;
+    return launch_render_pass(sc, b, traversal, block, d_out, nullptr, d_work, stream);
+}
+
+hipError_t launch_render_pass(const DevScene& sc, const FrameParams& fp, int traversal, int block, float* d_out,
                          unsigned long long* d_counts, unsigned int* d_work, hipStream_t stream) {
     if (traversal == TRAV_REF) {
         return d_counts ? launch_t<TRAV_REF, true, false>(sc, fp, block, d_out, d_counts, d_work, stream)

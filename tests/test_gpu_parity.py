@@ -696,3 +696,45 @@ def test_fixed_point_samples_render_identically(kl, case):
     assert c1["rays"] <= c0["rays"]
     with pytest.raises(_native.NativeError, match="fixed_point"):
         kl.native.set_option("fixed_point", 2)
+
+
+@pytest.mark.parametrize("case,pilot", [("cornell_128_s16", 4), ("cornell_128_s16", 1), ("monkey_c3_64_s4", 2),
+                                        ("serre_96x54_s4", 3), ("proto_64_s4", 1)])
+def test_two_pass_pilot_renders_identically(kl, case, pilot):
+    """pilot: pass 1 renders each pixel's first `pilot` samples and saves its state, pass 2 continues
+    the pixels in descending pilot cost.  Every pixel's samples run in the same order, so the frame
+    equals the one-pass frame and the oracle."""
+    sc, cam, env, npix, spp, mb, ibl = W.PARITY_CASES[case].inputs()
+    try:
+        kl.native.set_option("pilot", 0)
+        one = _launch(kl, sc, cam, env, npix, spp, mb, ibl, "fast")
+        kl.native.set_option("pilot", pilot)
+        two = _launch(kl, sc, cam, env, npix, spp, mb, ibl, "fast")
+    finally:
+        kl.native.set_option("pilot", -1)
+    np.testing.assert_array_equal(two, one)
+    np.testing.assert_array_equal(two, _oracle(sc, cam, env, npix, spp, mb, ibl))
+    with pytest.raises(_native.NativeError, match="pilot"):
+        kl.native.set_option("pilot", -2)
+
+
+@pytest.mark.parametrize("config,pilot,spp", [("C2", 8, 64), ("C3", -1, 32), ("C4", -1, 16)])
+def test_two_pass_pilot_full_frame(kl, config, pilot, spp):
+    """The pilot pass on the full-size frames -- automatic (spp / 8 samples, per-pixel order) for the
+    tree walk, explicit for the brute-force path (wave-sized chunks): bit-identical to one pass."""
+    import torch
+    sc, cam, env, npix, _, mb, ibl = W.CONFIGS[config].inputs()
+    ctx = _native.Context(device_ids=[0])
+    try:
+        ctx.set_scene(sc.V_p, sc.V_n, sc.V_uv, sc.faceData, sc.materialData, sc.BVH.exportArray)
+        ctx.set_env(ibl)
+        out = {}
+        for pv in (0, pilot):
+            ctx.set_option("pilot", pv)
+            t = torch.empty(3 * npix, dtype=torch.float32, device="cuda")
+            ctx.render_device(cam, env, npix, spp, mb, 0, 1, t.data_ptr())
+            torch.cuda.synchronize()
+            out[pv] = t.cpu().numpy()
+    finally:
+        ctx.close()
+    np.testing.assert_array_equal(out[pilot], out[0])
