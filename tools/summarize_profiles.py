@@ -1,6 +1,6 @@
 """Summarise the rocprofv3 output of tools/run_profiles.sh into profiles/ (committed evidence).
 
-    python tools/summarize_profiles.py gpurun_out/prof_C2 TAG WORKLOAD
+    python tools/summarize_profiles.py gpurun_out/prof_C2 TAG WORKLOAD [FRAMES]
 
 Writes profiles/TAG_kernel_stats_WORKLOAD.csv (the --stats table of the kernel-trace run) and
 profiles/TAG_pmc_WORKLOAD.json: per-launch means of every counter of the render kernel, and
@@ -33,7 +33,10 @@ def _rows(pattern):
     return out
 
 
-def main(prof, tag, workload, kernel=KERNEL):
+def main(prof, tag, workload, frames=None, kernel=KERNEL):
+    """frames: frames the profiled run rendered (bench warmup + steps).  A frame may take several
+    dispatches of the render kernel (two-pass launches, option "pilot"); every *_per_launch value and
+    kernel_avg_ms are then per frame (totals / frames).  Default: one dispatch per frame."""
     os.makedirs(os.path.join(ROOT, "profiles"), exist_ok=True)
     stats = glob.glob(os.path.join(prof, "kt", "*kernel_stats.csv"))
     s = {"workload": workload, "kernel": kernel, "source": "rocprofv3 (tools/run_profiles.sh)"}
@@ -43,14 +46,16 @@ def main(prof, tag, workload, kernel=KERNEL):
             if re.search(kernel, r["Name"]):
                 s["kernel_name"] = r["Name"][:120]
                 s["kernel_calls"] = int(r["Calls"])
-                s["kernel_avg_ms"] = float(r["AverageNs"]) / 1e6
+                s["frames"] = int(frames) if frames else int(r["Calls"])
+                s["kernel_avg_ms"] = float(r["TotalDurationNs"]) / 1e6 / s["frames"]
     counters = {}
     for sub in ("fetch", "write", "dram", "sq"):
         for r in _rows(os.path.join(prof, sub, "*counter_collection.csv")):
             if re.search(kernel, r["Kernel_Name"]):
                 counters.setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))
+    per = s.get("kernel_calls", 1) / max(1, s.get("frames", 1))   # dispatches per frame
     for k, v in sorted(counters.items()):
-        s[k + "_per_launch"] = float(np.mean(v))
+        s[k + "_per_launch"] = float(np.mean(v)) * per
         s[k + "_launches"] = len(v)
     g = lambda k: s.get(k + "_per_launch")  # noqa: E731
     if g("FETCH_SIZE") is not None and g("WRITE_SIZE") is not None:
@@ -71,4 +76,4 @@ def main(prof, tag, workload, kernel=KERNEL):
 
 
 if __name__ == "__main__":
-    main(*sys.argv[1:4])
+    main(*sys.argv[1:5])
