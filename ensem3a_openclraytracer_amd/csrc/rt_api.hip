@@ -102,6 +102,8 @@ struct rt_ctx {
     int bvh_width = 0;  // FAST tree walk: 2 = BVH2 nodes, 4 = the 4-wide quantised layout, 0 = auto (option "bvh_width")
     int fixed_point = 1;  // sum the repeats of a sample that draws no random number (FrameParams::fixed_point)
     int pilot = -1;       // two-pass launches: pilot samples per pixel (0 = one pass, -1 = auto; FrameParams::pilot)
+    int pilot_chunk = 0;  // pixels ordered together (0 = auto: 64 brute force, 1 tree walk)
+    int pilot_levels = 0; // cost bins of the order (0 = auto: 256)
     std::string err;
 };
 
@@ -650,6 +652,8 @@ int check_frame(rt_ctx* ctx, const float* cam, const float* env, int64_t npix, i
     fp->fixed_point = ctx->fixed_point;
     fp->pass = 0;
     fp->pilot = 0;
+    fp->pilot_chunk = 1;
+    fp->pilot_levels = 256;
     fp->pilot_state = nullptr;
     fp->pilot_cost = nullptr;
     fp->pilot_order = nullptr;
@@ -795,6 +799,16 @@ int rt_set_option(rt_ctx* ctx, const char* key, int64_t value) {
     if (!std::strcmp(key, "pilot")) {
         if (value < -1 || value > (1 << 20)) return set_err(ctx, RT_ERR_ARG, "pilot must be -1 (auto), 0 (off) or a sample count");
         ctx->pilot = (int)value;
+        return RT_OK;
+    }
+    if (!std::strcmp(key, "pilot_chunk")) {
+        if (value < 0 || value > 4096) return set_err(ctx, RT_ERR_ARG, "pilot_chunk must be in 0..4096 (0 = auto)");
+        ctx->pilot_chunk = (int)value;
+        return RT_OK;
+    }
+    if (!std::strcmp(key, "pilot_levels")) {
+        if (value != 0 && (value < 2 || value > 256)) return set_err(ctx, RT_ERR_ARG, "pilot_levels must be 0 (auto) or 2..256");
+        ctx->pilot_levels = (int)value;
         return RT_OK;
     }
     if (!std::strcmp(key, "fixed_point")) {
@@ -969,12 +983,15 @@ hipError_t setup_pilot(rt_ctx* ctx, Device& d, rt::FrameParams& fp) {
     }
     if (k >= fp.spp) return hipSuccess;
     const size_t n = (size_t)fp.nloc;
-    // state 32 B | cost 4 B | order 4 B per pixel, cost histogram + offsets (2 x 256), and the chunk
-    // costs + chunk order (at most one chunk per pixel: the tree walk orders single pixels)
-    hipError_t e = ensure(d.pilot, n * 32 + n * 8 + 2 * 256 * sizeof(uint32_t) + 2 * (n + 1) * sizeof(uint32_t));
+    // state 32 B | cost 4 B | order 4 B per pixel, bin totals + offsets (2 x 256), the chunk costs +
+    // chunk order (at most one chunk per pixel) and the sort's segment histograms (256 per 256 chunks)
+    hipError_t e = ensure(d.pilot, n * 40 + 2 * 256 * sizeof(uint32_t) + 2 * (n + 1) * sizeof(uint32_t) +
+                                       (n + 256) * sizeof(uint32_t));
     if (e != hipSuccess) return e;
     char* base = (char*)d.pilot.p;
     fp.pilot = k;
+    fp.pilot_chunk = ctx->pilot_chunk > 0 ? ctx->pilot_chunk : (ctx->hs.nbrute > 0 ? 64 : 1);
+    fp.pilot_levels = ctx->pilot_levels > 0 ? ctx->pilot_levels : 256;
     fp.pilot_state = (float4*)base;
     fp.pilot_cost = (uint32_t*)(base + n * 32);
     fp.pilot_order = (const uint32_t*)(base + n * 36);

@@ -111,6 +111,8 @@ struct FrameParams {
     // short ones.  pass 0 = one pass.
     int32_t pass;
     int32_t pilot;
+    int32_t pilot_chunk;   // pixels ordered together (consecutive tile pixels; 1 = single pixels)
+    int32_t pilot_levels;  // cost bins of the order (2..256); within a bin the chunks keep tile order
     float4* pilot_state;
     uint32_t* pilot_cost;
     const uint32_t* pilot_order;

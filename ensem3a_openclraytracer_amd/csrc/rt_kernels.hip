@@ -1948,20 +1948,51 @@ __global__ void pilot_chunk_kernel(const uint32_t* __restrict__ cost, int64_t nf
     }
 }
 
-__device__ __forceinline__ uint32_t cost_bin(uint32_t v, uint32_t scale) {
-    return min((uint32_t)(kCostBins - 1), (uint32_t)(((uint64_t)v * scale) >> 16));
+__device__ __forceinline__ uint32_t cost_bin(uint32_t v, uint32_t scale, uint32_t maxbin) {
+    return min(maxbin, (uint32_t)(((uint64_t)v * scale) >> 16));
 }
 
-__global__ void pilot_hist_kernel(const uint32_t* __restrict__ ccost, int64_t n, uint32_t scale,
-                                  uint32_t* __restrict__ hist) {
+// Stable counting sort of the chunks by cost bin (descending bins, tile order within a bin, so the
+// pixels of one bin keep their raster order and a wave's lanes stay on nearby pixels), over segments
+// of kSortSeg chunks: per-segment histograms (bin-major), their per-bin exclusive scan, the bin
+// offsets, then each chunk's place = bin offset + segment offset + its rank among the segment's
+// chunks of the same bin.
+constexpr int kSortSeg = kCostBins;
+
+__global__ void pilot_seg_hist_kernel(const uint32_t* __restrict__ ccost, int64_t n, int64_t nseg, uint32_t scale,
+                                      uint32_t maxbin, uint32_t* __restrict__ seghist) {
     __shared__ uint32_t h[kCostBins];
-    for (int b = threadIdx.x; b < kCostBins; b += blockDim.x) h[b] = 0;
+    const int64_t seg = blockIdx.x;
+    h[threadIdx.x] = 0;
     __syncthreads();
-    for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < n; q += (int64_t)gridDim.x * blockDim.x)
-        atomicAdd(&h[cost_bin(ccost[q], scale)], 1u);
+    const int64_t q = seg * kSortSeg + threadIdx.x;
+    if (q < n) atomicAdd(&h[cost_bin(ccost[q], scale, maxbin)], 1u);
     __syncthreads();
-    for (int b = threadIdx.x; b < kCostBins; b += blockDim.x)
-        if (h[b]) atomicAdd(&hist[b], h[b]);
+    seghist[threadIdx.x * nseg + seg] = h[threadIdx.x];
+}
+
+// one block per bin: exclusive scan of the bin's row of seghist in place, the row total to total[bin]
+__global__ void pilot_seg_scan_kernel(uint32_t* __restrict__ seghist, int64_t nseg, uint32_t* __restrict__ total) {
+    __shared__ uint32_t t[kCostBins];
+    uint32_t* row = seghist + (int64_t)blockIdx.x * nseg;
+    const int i0 = threadIdx.x;
+    uint32_t carry = 0;
+    for (int64_t base = 0; base < nseg; base += kCostBins) {
+        const int64_t i = base + i0;
+        const uint32_t v = i < nseg ? row[i] : 0u;
+        t[i0] = v;
+        __syncthreads();
+        for (int off = 1; off < kCostBins; off <<= 1) {
+            const uint32_t a = i0 >= off ? t[i0 - off] : 0u;
+            __syncthreads();
+            t[i0] += a;
+            __syncthreads();
+        }
+        if (i < nseg) row[i] = carry + t[i0] - v;
+        carry += t[kCostBins - 1];
+        __syncthreads();
+    }
+    if (i0 == 0) total[blockIdx.x] = carry;
 }
 
 // offs[b] = number of chunks in bins above b (descending cost order); one block of kCostBins threads
@@ -1975,10 +2006,19 @@ __global__ void pilot_scan_kernel(const uint32_t* __restrict__ hist, uint32_t* _
     offs[b] = above;
 }
 
-__global__ void pilot_scatter_kernel(const uint32_t* __restrict__ ccost, int64_t n, uint32_t scale,
-                                     uint32_t* __restrict__ offs, uint32_t* __restrict__ corder) {
-    for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < n; q += (int64_t)gridDim.x * blockDim.x)
-        corder[atomicAdd(&offs[cost_bin(ccost[q], scale)], 1u)] = (uint32_t)q;
+__global__ void pilot_seg_scatter_kernel(const uint32_t* __restrict__ ccost, int64_t n, int64_t nseg, uint32_t scale,
+                                         uint32_t maxbin, const uint32_t* __restrict__ seghist,
+                                         const uint32_t* __restrict__ offs, uint32_t* __restrict__ corder) {
+    __shared__ uint32_t bins[kSortSeg];
+    const int64_t seg = blockIdx.x;
+    const int64_t q = seg * kSortSeg + threadIdx.x;
+    const uint32_t b = q < n ? cost_bin(ccost[q], scale, maxbin) : 0xffffffffu;
+    bins[threadIdx.x] = b;
+    __syncthreads();
+    if (q >= n) return;
+    uint32_t rank = 0;
+    for (int j = 0; j < (int)threadIdx.x; ++j) rank += bins[j] == b ? 1u : 0u;
+    corder[offs[b] + seghist[(int64_t)b * nseg + seg] + rank] = (uint32_t)q;
 }
 
 // pixel order: the full chunks in cost order, then the last partial chunk (if any) in place
@@ -2003,26 +2043,32 @@ hipError_t launch_render(const DevScene& sc, const FrameParams& fp, int traversa
     a.pass = 1;
     hipError_t e = launch_render_pass(sc, a, traversal, block, d_out, nullptr, d_work, stream);
     if (e != hipSuccess) return e;
-    // scratch after the pixel order (rt_api.hip setup_pilot): hist | offs | chunk costs | chunk order
+    // scratch after the pixel order (rt_api.hip setup_pilot): bin totals | offs | chunk costs |
+    // chunk order | segment histograms
     uint32_t* order = const_cast<uint32_t*>(fp.pilot_order);
-    uint32_t* hist = order + fp.nloc;
-    uint32_t* offs = hist + kCostBins;
-    const int chunk = sc.nbrute > 0 ? 64 : 1;
+    uint32_t* total = order + fp.nloc;
+    uint32_t* offs = total + kCostBins;
+    const int chunk = std::max(fp.pilot_chunk, 1);
     const int64_t nfull = fp.nloc / chunk;
+    const int64_t nseg = (nfull + kSortSeg - 1) / kSortSeg;
     uint32_t* ccost = offs + kCostBins;
     uint32_t* corder = ccost + nfull;
-    // cost bins over a chunk's rays up to 2 (maxBounce + 1) rays per pilot sample per pixel
+    uint32_t* seghist = corder + nfull;
+    // `levels` cost bins over a chunk's rays up to 2 (maxBounce + 1) rays per pilot sample per pixel
+    const int levels = std::min(std::max(fp.pilot_levels, 2), kCostBins);
     const uint64_t top = (uint64_t)chunk * fp.pilot * 2u * (uint64_t)(std::max(fp.max_bounce, 0) + 1);
-    const uint32_t scale = (uint32_t)std::max<uint64_t>(1, ((uint64_t)kCostBins << 16) / std::max<uint64_t>(top, 1));
-    e = hipMemsetAsync(hist, 0, kCostBins * sizeof(uint32_t), stream);
-    if (e != hipSuccess) return e;
+    const uint32_t scale = (uint32_t)std::max<uint64_t>(1, ((uint64_t)levels << 16) / std::max<uint64_t>(top, 1));
+    const uint32_t maxbin = (uint32_t)levels - 1;
     const unsigned gc = (unsigned)std::max<int64_t>(1, std::min<int64_t>((nfull + 255) / 256, 2048));
     const unsigned gp = (unsigned)std::min<int64_t>((fp.nloc + 255) / 256, 2048);
     if (nfull > 0) {
         hipLaunchKernelGGL(pilot_chunk_kernel, dim3(gc), dim3(256), 0, stream, fp.pilot_cost, nfull, chunk, ccost);
-        hipLaunchKernelGGL(pilot_hist_kernel, dim3(gc), dim3(256), 0, stream, ccost, nfull, scale, hist);
-        hipLaunchKernelGGL(pilot_scan_kernel, dim3(1), dim3(kCostBins), 0, stream, hist, offs);
-        hipLaunchKernelGGL(pilot_scatter_kernel, dim3(gc), dim3(256), 0, stream, ccost, nfull, scale, offs, corder);
+        hipLaunchKernelGGL(pilot_seg_hist_kernel, dim3((unsigned)nseg), dim3(kSortSeg), 0, stream, ccost, nfull, nseg,
+                           scale, maxbin, seghist);
+        hipLaunchKernelGGL(pilot_seg_scan_kernel, dim3(kCostBins), dim3(kCostBins), 0, stream, seghist, nseg, total);
+        hipLaunchKernelGGL(pilot_scan_kernel, dim3(1), dim3(kCostBins), 0, stream, total, offs);
+        hipLaunchKernelGGL(pilot_seg_scatter_kernel, dim3((unsigned)nseg), dim3(kSortSeg), 0, stream, ccost, nfull,
+                           nseg, scale, maxbin, seghist, offs, corder);
     }
     hipLaunchKernelGGL(pilot_expand_kernel, dim3(gp), dim3(256), 0, stream, corder, nfull, chunk, fp.nloc, order);
     FrameParams b = fp;

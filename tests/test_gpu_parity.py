@@ -718,6 +718,28 @@ def test_two_pass_pilot_renders_identically(kl, case, pilot):
         kl.native.set_option("pilot", -2)
 
 
+@pytest.mark.parametrize("case,chunk,levels", [("cornell_128_s16", 1, 4), ("cornell_128_s16", 100, 256),
+                                               ("serre_96x54_s4", 64, 2), ("monkey_c3_64_s4", 7, 33)])
+def test_two_pass_pilot_order_options(kl, case, chunk, levels):
+    """pilot_chunk / pilot_levels only change the pass-2 order (a stable counting sort of chunks of
+    consecutive pixels by cost bin, partial last chunk in place): every pixel is continued once."""
+    sc, cam, env, npix, spp, mb, ibl = W.PARITY_CASES[case].inputs()
+    try:
+        kl.native.set_option("pilot", 2)
+        kl.native.set_option("pilot_chunk", chunk)
+        kl.native.set_option("pilot_levels", levels)
+        two = _launch(kl, sc, cam, env, npix, spp, mb, ibl, "fast")
+    finally:
+        kl.native.set_option("pilot", -1)
+        kl.native.set_option("pilot_chunk", 0)
+        kl.native.set_option("pilot_levels", 0)
+    np.testing.assert_array_equal(two, _oracle(sc, cam, env, npix, spp, mb, ibl))
+    with pytest.raises(_native.NativeError, match="pilot_levels"):
+        kl.native.set_option("pilot_levels", 1)
+    with pytest.raises(_native.NativeError, match="pilot_chunk"):
+        kl.native.set_option("pilot_chunk", -1)
+
+
 @pytest.mark.parametrize("config,pilot,spp", [("C2", 8, 64), ("C3", -1, 32), ("C4", -1, 16)])
 def test_two_pass_pilot_full_frame(kl, config, pilot, spp):
     """The pilot pass on the full-size frames -- automatic (spp / 8 samples, per-pixel order) for the
