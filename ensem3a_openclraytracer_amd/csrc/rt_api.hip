@@ -104,6 +104,7 @@ struct rt_ctx {
     int pilot = -1;       // two-pass launches: pilot samples per pixel (0 = one pass, -1 = auto; FrameParams::pilot)
     int pilot_chunk = 0;  // pixels ordered together (0 = auto: 64 brute force, 1 tree walk)
     int pilot_levels = 0; // cost bins of the order (0 = auto: 256)
+    int stack_lds = 0;    // FAST stack entries per lane kept in LDS (0 = auto: rt::kStackLds)
     std::string err;
 };
 
@@ -556,10 +557,11 @@ void pack_checked(HostScene& hs, const float* bvh9, int64_t nb, int64_t ntri, in
     if (hs.brute_box.empty()) hs.brute_box.assign(8 * rt::kBoxGroup, 1e30f);
 }
 
-// HBM part of the FAST traversal stack: (depth - kStackLds) entries for every lane a
-// persistent render grid can hold.
+// HBM part of the FAST traversal stack: (depth - kStackLdsMin) entries for every lane a
+// persistent render grid can hold (option "stack_lds" may keep as few as kStackLdsMin in LDS).
+constexpr int kStackLdsMin = 8;
 hipError_t ensure_stack_ovf(Device& d, const HostScene& hs) {
-    const int64_t extra = (int64_t)std::max(hs.depth, hs.wdepth) - rt::kStackLds;
+    const int64_t extra = (int64_t)std::max(hs.depth, hs.wdepth) - kStackLdsMin;
     if (extra <= 0) return hipSuccess;
     return ensure(d.stack_ovf, (size_t)std::max(d.cus, 1) * rt::kMaxLanesPerCu * (size_t)extra * sizeof(int2));
 }
@@ -619,7 +621,7 @@ rt::DevScene dev_scene(const rt_ctx* ctx, const Device& d) {
     s.brute_box = (const float4*)d.brute_box.p;
     s.nbrute = ctx->hs.nbrute;
     s.nbox = ctx->hs.nbox;
-    s.stack_lds = std::min<int32_t>(s.depth > 0 ? s.depth : 1, rt::kStackLds);
+    s.stack_lds = std::min<int32_t>(s.depth > 0 ? s.depth : 1, ctx->stack_lds > 0 ? ctx->stack_lds : rt::kStackLds);
     s.stack_ovf = (int2*)d.stack_ovf.p;
     return s;
 }
@@ -809,6 +811,12 @@ int rt_set_option(rt_ctx* ctx, const char* key, int64_t value) {
     if (!std::strcmp(key, "pilot_levels")) {
         if (value != 0 && (value < 2 || value > 256)) return set_err(ctx, RT_ERR_ARG, "pilot_levels must be 0 (auto) or 2..256");
         ctx->pilot_levels = (int)value;
+        return RT_OK;
+    }
+    if (!std::strcmp(key, "stack_lds")) {
+        if (value != 0 && (value < kStackLdsMin || value > rt::kStackLds))
+            return set_err(ctx, RT_ERR_ARG, "stack_lds must be 0 (auto) or %d..%d", kStackLdsMin, rt::kStackLds);
+        ctx->stack_lds = (int)value;
         return RT_OK;
     }
     if (!std::strcmp(key, "fixed_point")) {

@@ -1413,8 +1413,16 @@ __device__ __forceinline__ bool wide_round(FastRay& R, const char* nb, const cha
 // 944 Msamples/s there)
 constexpr size_t kStepMaxBytes = 16u << 20;
 
+#ifndef RT_RESUME_WAVES
+#define RT_RESUME_WAVES 0
+#endif
+#if RT_RESUME_WAVES > 0
+#define RESUME_OCC __attribute__((amdgpu_waves_per_eu(RT_RESUME_WAVES)))
+#else
+#define RESUME_OCC
+#endif
 template <bool COUNT, bool LOG, bool SMEM, bool OVF, bool STEP, bool WIDE>
-__global__ void __launch_bounds__(256) render_resume_kernel(DevScene S, FrameParams F, float* __restrict__ out,
+__global__ void __launch_bounds__(256) RESUME_OCC render_resume_kernel(DevScene S, FrameParams F, float* __restrict__ out,
                                                       unsigned long long* __restrict__ counts,
                                                       unsigned int* __restrict__ work_counter,
                                                       const LaunchConst* __restrict__ lconst) {
