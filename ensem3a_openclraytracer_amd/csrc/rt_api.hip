@@ -104,7 +104,7 @@ struct rt_ctx {
     int pilot = -1;       // two-pass launches: pilot samples per pixel (0 = one pass, -1 = auto; FrameParams::pilot)
     int pilot_chunk = 0;  // pixels ordered together (0 = auto: 64 brute force, 1 tree walk)
     int pilot_levels = 0; // cost bins of the order (0 = auto: 256)
-    int stack_lds = 0;    // FAST stack entries per lane kept in LDS (0 = auto: rt::kStackLds)
+    int stack_lds = 0;    // FAST stack entries per lane kept in LDS (0 = auto: rt::kStackLds, kStackLdsWide)
     std::string err;
 };
 
@@ -621,7 +621,8 @@ rt::DevScene dev_scene(const rt_ctx* ctx, const Device& d) {
     s.brute_box = (const float4*)d.brute_box.p;
     s.nbrute = ctx->hs.nbrute;
     s.nbox = ctx->hs.nbox;
-    s.stack_lds = std::min<int32_t>(s.depth > 0 ? s.depth : 1, ctx->stack_lds > 0 ? ctx->stack_lds : rt::kStackLds);
+    s.stack_lds = std::min<int32_t>(s.depth > 0 ? s.depth : 1,
+                                    ctx->stack_lds > 0 ? ctx->stack_lds : wide ? rt::kStackLdsWide : rt::kStackLds);
     s.stack_ovf = (int2*)d.stack_ovf.p;
     return s;
 }

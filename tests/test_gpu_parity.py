@@ -718,6 +718,25 @@ def test_two_pass_pilot_renders_identically(kl, case, pilot):
         kl.native.set_option("pilot", -2)
 
 
+@pytest.mark.parametrize("case", ["monkey_c3_64_s4", "serre_96x54_s4"])
+def test_stack_lds_entries_render_identically(kl, case):
+    """stack_lds: how many FAST stack entries per lane live in LDS (deeper ones spill to the HBM
+    overflow buffer; the 4-wide walk defaults to kStackLdsWide).  8 forces the spill path on these
+    trees; the frame is the oracle's either way."""
+    sc, cam, env, npix, spp, mb, ibl = W.PARITY_CASES[case].inputs()
+    want = _oracle(sc, cam, env, npix, spp, mb, ibl)
+    try:
+        for width, entries in ((2, 8), (4, 8), (4, 20)):
+            kl.native.set_option("bvh_width", width)
+            kl.native.set_option("stack_lds", entries)
+            np.testing.assert_array_equal(_launch(kl, sc, cam, env, npix, spp, mb, ibl, "fast"), want)
+    finally:
+        kl.native.set_option("bvh_width", 0)
+        kl.native.set_option("stack_lds", 0)
+    with pytest.raises(_native.NativeError, match="stack_lds"):
+        kl.native.set_option("stack_lds", 7)
+
+
 @pytest.mark.parametrize("case,chunk,levels", [("cornell_128_s16", 1, 4), ("cornell_128_s16", 100, 256),
                                                ("serre_96x54_s4", 64, 2), ("monkey_c3_64_s4", 7, 33)])
 def test_two_pass_pilot_order_options(kl, case, chunk, levels):
