@@ -199,6 +199,36 @@ def time_config(ctx_factory, name: str, steps: int, warmup: int):
             "valu_frac": rf["frac"] if rf["bound"] == "valu" else rf["other_bound"]["frac"]}
 
 
+def two_frames_in_flight(ctx, make_ctx, scene, ibl, cam, env, npix, spp, mb, steps, warmup) -> dict:
+    """Frames of a sequence (an animation, or a UI re-rendering) rendered on two contexts and two
+    streams alternately, so that one frame's kernel fills the CUs its predecessor's tail leaves idle
+    (frame tail).  Reported beside the headline, never as `value`: the headline renders
+    one frame at a time, as launch_Raytracing does."""
+    import torch
+    ctx2 = make_ctx()
+    try:
+        ctx2.set_scene(scene.V_p, scene.V_n, scene.V_uv, scene.faceData, scene.materialData, scene.BVH.exportArray)
+        ctx2.set_env(ibl)
+        lanes = [(ctx, torch.cuda.Stream()), (ctx2, torch.cuda.Stream())]
+        outs = [torch.empty(3 * npix, dtype=torch.float32, device="cuda") for _ in lanes]
+
+        def run(n):
+            for f in range(n):
+                c, s = lanes[f % 2]
+                c.render_device(cam, env, npix, spp, mb, 0, 1, outs[f % 2].data_ptr(), s.cuda_stream)
+            torch.cuda.synchronize()
+
+        run(max(warmup, 2))
+        t0 = time.perf_counter()
+        run(steps)
+        dt = (time.perf_counter() - t0) / steps
+    finally:
+        ctx2.close()
+    return {"value": round(npix * spp / dt / 1e6, 3), "unit": "Msamples/s", "ms_per_frame": round(dt * 1e3, 4),
+            "steps": steps, "what": "consecutive frames alternating over two contexts / streams (frame k+1 starts "
+                                    "while frame k drains); not the headline, which renders one frame at a time"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -366,6 +396,9 @@ def main():
                                      "ms_per_frame": round(dt * 1e3, 3), "steps": args.steps,
                                      "what": "rt_render (launch_Raytracing's C-ABI): kernel + copy of the frame "
                                              "into caller memory, scene already uploaded"}
+        if world == 1 and not args.no_extra:
+            line["two_frames_in_flight"] = two_frames_in_flight(ctx, make_ctx, scene, ibl, cam, env, npix, spp, mb,
+                                                                args.steps, args.warmup)
         if world == 1 and not args.no_extra and args.config == "C2":
             ctx.close()
             ctx = None
