@@ -1464,10 +1464,11 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WIDE ?
     rtm_f3 cd = rtm_v3(0, 0, 0);              // camera ray direction (origin = C.position)
     float kc = 1000.0f;                       // cached primary hit (Raytracing.cl:186-187)
     int tc = -1;
-    rtm_f3 Ro = rtm_v3(0, 0, 0), Rd = rtm_v3(0, 0, 0), so = rtm_v3(1, 1, 1);
-    float k = 1000.0f;
+    // the ray being shaded is not kept: at bounce 0 it is the camera ray (C.position, cd, hit kc),
+    // later the bounce ray just traced (T.o, T.d, hit T.bk) -- fewer registers live across traversal
+    rtm_f3 so = rtm_v3(1, 1, 1);
     int tri = -1, j = 0;
-    rtm_f3 Bo = rtm_v3(0, 0, 0), Bd = rtm_v3(0, 0, 0);
+    rtm_f3 Bd = rtm_v3(0, 0, 0);   // bounce direction (its origin is T.o while it and the sun ray are traced)
     rtm_f3 acc = rtm_v3(0, 0, 0);
     int s = 0;
     bool drew = false;   // the current sample has drawn random numbers (a diffuse or glossy bounce)
@@ -1496,7 +1497,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WIDE ?
         // ends in a store the compiler could merge with the pixel store (that would force the path
         // state into scratch memory through a generic pointer)
         phase = (s >= spp || stop) ? FETCH : PREP;
-        Ro = C.position; Rd = cd; tri = tc; k = kc; j = 0;
+        tri = tc; j = 0;
         so = rtm_v3(1, 1, 1);
         drew = false;
     };
@@ -1550,7 +1551,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WIDE ?
                         seed1 = __float_as_uint(b.y);
                         tc = __float_as_int(b.z);
                         s = __float_as_int(b.w);
-                        Ro = C.position; Rd = cd; tri = tc; k = kc; j = 0;
+                        tri = tc; j = 0;
                         so = rtm_v3(1, 1, 1);
                         drew = false;
                         phase = s >= spp ? FETCH : PREP;   // finished in pass 1: already written
@@ -1572,7 +1573,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WIDE ?
             if (phase == PRIMARY) {
                 tc = h.tri;
                 kc = h.k;
-                Ro = C.position; Rd = cd; tri = tc; k = kc; j = 0;
+                tri = tc; j = 0;
                 so = rtm_v3(1, 1, 1);
                 drew = false;
                 phase = PREP;
@@ -1583,10 +1584,10 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WIDE ?
             } else if (phase == BOUNCE) {
                 if (LOG && logme) {
                     const int hm = h.tri >= 0 ? __float_as_int(S.tri_shade[h.tri].w) : 0;
-                    log_event(F, 1.0f, j, Bo, Bd, h.tri >= 0 ? h.k : -1.0f, hm, so);
+                    log_event(F, 1.0f, j, T.o, Bd, h.tri >= 0 ? h.k : -1.0f, hm, so);
                 }
                 if (h.tri >= 0) {
-                    Ro = Bo; Rd = Bd; tri = h.tri; k = h.k;
+                    tri = h.tri;
                     const Mat bm = load_mat(S.mat, __float_as_int(S.tri_shade[h.tri].w));
                     if (bm.type != 0) {
                         if (j == maxB) {
@@ -1607,7 +1608,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WIDE ?
                     // unlit sun (FrameParams::sun_skip): the shadow ray cannot change the sample; it is not
                     // traced and the sun term below runs now with h, the bounce ray's miss
                     if (!F.sun_skip) {
-                        start(Bo, C.sun);
+                        start(T.o, C.sun);
                         T.any = F.sun_any != 0;
                         if (!tracing) continue;  // unreachable in practice (root box always hit from inside)
                     }
@@ -1616,7 +1617,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WIDE ?
             if (phase == SUN && !tracing) {  // Raytracing.cl:125-137
                 if (LOG && logme) {
                     const int hm = h.tri >= 0 ? __float_as_int(S.tri_shade[h.tri].w) : 0;
-                    log_event(F, 2.0f, j, Bo, C.sun, h.tri >= 0 ? h.k : -1.0f, hm, so);
+                    log_event(F, 2.0f, j, T.o, C.sun, h.tri >= 0 ? h.k : -1.0f, hm, so);
                 }
                 rtm_f3 sunLight = rtm_v3(0, 0, 0);
                 if (COUNT) c.sun++;
@@ -1633,6 +1634,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WIDE ?
             }
             // naiveGI loop heads (Raytracing.cl:46-79) until a ray is needed or the pixel is done
             while (phase == PREP) {
+                const bool cam = j == 0;
+                const rtm_f3 Ro = cam ? C.position : T.o, Rd = cam ? cd : T.d;
+                const float k = cam ? kc : T.bk;
                 if (j > maxB) {
                     repeat_fixed();
                     finish_sample();   // naiveGI's loop never entered (maxBounce < 0): the sample stays 1
@@ -1666,7 +1670,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WIDE ?
                             invPdf = 1.0f / rtm_fabs(rtm_dot(Bd, nn));
                         }
                         const rtm_f3 nd = rtm_normalize(Rd);
-                        Bo = rtm_v3(fmaf(nd.x, k, Ro.x), fmaf(nd.y, k, Ro.y), fmaf(nd.z, k, Ro.z));
+                        const rtm_f3 Bo = rtm_v3(fmaf(nd.x, k, Ro.x), fmaf(nd.y, k, Ro.y), fmaf(nd.z, k, Ro.z));
                         // attenuation depends only on pre-trace values (Raytracing.cl:86-87): apply now
                         const float att = invPdf * rtm_fabs(rtm_dot(Bd, nn));
                         so = rtm_scale(rtm_mul(so, brdf), att);
