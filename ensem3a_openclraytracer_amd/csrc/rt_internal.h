@@ -8,10 +8,10 @@ namespace rt {
 
 // LDS entries of the FAST traversal stack per lane (int2 each); deeper entries spill to HBM.
 constexpr int kStackLds = 20;
-// ... and on the 4-wide walk, whose kernel runs 5 waves per SIMD (render_resume_kernel): 12 entries
-// (96 B per lane) leave the LDS room for them (C5 6,555 ms vs 6,939 with 16 entries, 7,214 with 20
-// at 4 waves)
-constexpr int kStackLdsWide = 12;
+// ... and on the 4-wide walk, whose kernel runs 7 waves per SIMD (render_resume_kernel, kWideWaves):
+// 11 entries (88 B per lane) leave the LDS room for them (C5 at 7 waves: 5,890 ms with 11 entries,
+// 5,915 with 10)
+constexpr int kStackLdsWide = 11;
 constexpr int kNodeF4 = 4;             // float4 per FAST BVH2 node (DevScene::nodes)
 constexpr int kMaxLanesPerCu = 2048;   // resident threads per CU (gfx950)
 constexpr int kBoxGroup = 4;           // leaf boxes per scalar load group of the brute-force loop (DevScene::brute_box)

@@ -1413,13 +1413,15 @@ __device__ __forceinline__ bool wide_round(FastRay& R, const char* nb, const cha
 // 944 Msamples/s there)
 constexpr size_t kStepMaxBytes = 16u << 20;
 
-// Occupancy: the 4-wide walk (C5: bound by the latency of L2 misses) runs 5 waves per SIMD -- the
-// register allocator keeps it at 96 VGPRs with a few spilled to scratch, and launch_fast keeps
-// kStackLdsWide stack entries per lane in LDS so that the LDS admits them (C5: 7,214 -> 6,555 ms);
-// the BVH2 walk (C3/C4: bound by the vector memory pipeline) keeps 4 waves, its 106 VGPRs and the
-// whole stack in LDS (5 waves with 16 LDS entries and a spilling stack: 150 -> 166 ms on C3).
+// Occupancy: the 4-wide walk (C5) is bound by the latency of dependent L2 misses, so it runs
+// kWideWaves waves per SIMD -- the register allocator keeps it at 72 VGPRs with some spilled to
+// scratch, and dev_scene keeps kStackLdsWide stack entries per lane in LDS so that the LDS admits
+// them.  C5 ms per frame at 4 / 5 / 6 / 7 / 8 waves: 7,214 / 6,432 / 6,045 / 5,890 / 6,040.  The
+// BVH2 walk (C3/C4) is bound by the vector memory pipeline and keeps 4 waves with its whole 20-entry
+// stack in LDS (5 waves with a 14-entry spilling stack: C3 149 -> 157 ms, C4 475 -> 502 ms).
+constexpr int kWideWaves = 7;
 template <bool COUNT, bool LOG, bool SMEM, bool OVF, bool STEP, bool WIDE>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WIDE ? 5 : 4))) render_resume_kernel(DevScene S, FrameParams F, float* __restrict__ out,
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WIDE ? kWideWaves : 4))) render_resume_kernel(DevScene S, FrameParams F, float* __restrict__ out,
                                                       unsigned long long* __restrict__ counts,
                                                       unsigned int* __restrict__ work_counter,
                                                       const LaunchConst* __restrict__ lconst) {
