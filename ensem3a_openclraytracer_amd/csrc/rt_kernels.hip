@@ -924,7 +924,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) r
     rtm_f3 cd = rtm_v3(0, 0, 0);              // camera ray direction (origin = C.position)
     float kc = 1000.0f;                       // cached primary hit
     int tc = -1;
-    rtm_f3 Ro = rtm_v3(0, 0, 0), Rd = rtm_v3(0, 0, 0), so = rtm_v3(1, 1, 1);
+    // the ray being shaded is not kept: at bounce 0 it is the camera ray (C.position, cd, hit kc),
+    // later the bounce ray just traced (Bo, Bd, hit k) -- fewer registers live across the trace
+    rtm_f3 so = rtm_v3(1, 1, 1);
     float k = 1000.0f;
     int tri = -1, j = 0;
     rtm_f3 Bo = rtm_v3(0, 0, 0), Bd = rtm_v3(0, 0, 0);
@@ -974,7 +976,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) r
                         seed1 = __float_as_uint(b.y);
                         tc = __float_as_int(b.z);
                         s = __float_as_int(b.w);
-                        Ro = C.position; Rd = cd; tri = tc; k = kc; j = 0;
+                        tri = tc; j = 0;
                         so = rtm_v3(1, 1, 1);
                         phase = s >= spp ? FETCH : PREP;   // finished in pass 1: already written
                     }
@@ -991,6 +993,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) r
         if (phase == PREP) {
             // naiveGI loop head for bounce j (Raytracing.cl:46-79); may complete samples without tracing
             bool done = true;
+            const bool cam = j == 0;
+            const rtm_f3 Ro = cam ? C.position : Bo, Rd = cam ? cd : Bd;
+            const float kh = cam ? kc : k;
             if (j > maxB) {
                 // naiveGI's loop never entered (maxBounce < 0): the sample stays 1
             } else if (tri < 0) {
@@ -1021,7 +1026,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) r
                         invPdf = 1.0f / rtm_fabs(rtm_dot(Bd, nn));
                     }
                     const rtm_f3 nd = rtm_normalize(Rd);
-                    Bo = rtm_v3(fmaf(nd.x, k, Ro.x), fmaf(nd.y, k, Ro.y), fmaf(nd.z, k, Ro.z));
+                    Bo = rtm_v3(fmaf(nd.x, kh, Ro.x), fmaf(nd.y, kh, Ro.y), fmaf(nd.z, kh, Ro.z));
                     // attenuation depends only on pre-trace values (Raytracing.cl:86-87): apply now
                     const float att = invPdf * rtm_fabs(rtm_dot(Bd, nn));
                     so = rtm_scale(rtm_mul(so, brdf), att);
@@ -1050,7 +1055,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) r
                     save_pilot();
                     phase = FETCH;
                 } else {
-                    Ro = C.position; Rd = cd; tri = tc; k = kc; j = 0;
+                    tri = tc; j = 0;
                     so = rtm_v3(1, 1, 1);
                 }
                 continue;
@@ -1066,7 +1071,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) r
         if (phase == PRIMARY) {
             tc = h.tri;
             kc = h.k;
-            Ro = C.position; Rd = cd; tri = tc; k = kc; j = 0;
+            tri = tc; j = 0;
             so = rtm_v3(1, 1, 1);
             phase = PREP;
             if (spp <= 0) {   // reference: output = 0/0 -> NaN -> clamp gives 1
@@ -1082,7 +1087,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) r
         int sun_hit = -2;   // the shadow ray's hit for the sun term below (-1 = miss; -2 = no sun term now)
         if (phase == BOUNCE) {
             if (h.tri >= 0) {
-                Ro = Bo; Rd = Bd; tri = h.tri; k = h.k;
+                tri = h.tri; k = h.k;
                 const Mat bm = load_mat(tmat, __float_as_int(tshade[h.tri].w));
                 if (bm.type != 0) {
                     if (j == maxB) {
@@ -1130,7 +1135,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) r
                 save_pilot();
                 phase = FETCH;
             } else {
-                Ro = C.position; Rd = cd; tri = tc; k = kc; j = 0;
+                tri = tc; j = 0;
                 so = rtm_v3(1, 1, 1);
                 phase = PREP;
             }
