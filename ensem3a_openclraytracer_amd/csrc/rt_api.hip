@@ -26,7 +26,10 @@
 #include "rt_internal.h"
 
 #ifndef RT_RESUME_MIN_DEFAULT
-#define RT_RESUME_MIN_DEFAULT 40  // FAST tree walk: resumable traversal threshold (rt_set_option "resume_min")
+// FAST tree walk: resumable traversal threshold (rt_set_option "resume_min"; -1 = auto): 40 on the
+// BVH2 walk (C3 / C4 ms at 32 / 40 / 48: 157 / 150 / 151, 480 / 473 / 477), 48 on the 4-wide walk
+// (C5 at 40 / 48 / 52 / 56: 5,918 / 5,799 / 5,849 / 5,991)
+constexpr int kResumeMinBvh2 = 40, kResumeMinWide = 48;
 #endif
 #ifndef RT_BRUTE_MAX_DEFAULT
 #define RT_BRUTE_MAX_DEFAULT 64   // FAST tests every triangle of scenes up to this size (rt_set_option "brute_max")
@@ -92,7 +95,7 @@ struct rt_ctx {
     int traversal = RT_TRAVERSAL_FAST;
     int bvh_layout = RT_BVH_SAH;
     int brute_max = RT_BRUTE_MAX_DEFAULT;
-    int resume_min = RT_RESUME_MIN_DEFAULT;
+    int resume_min = -1;
     int team = 0;  // brute-force lanes per pixel, 0 = auto
     int max_waves = 0;  // persistent grid cap in waves per SIMD, 0 = occupancy limit
     int step = 0;       // tree-walk traversal loop: 0 auto, 1 one item per step, 2 descend-until-leaf rounds
@@ -647,7 +650,7 @@ int check_frame(rt_ctx* ctx, const float* cam, const float* env, int64_t npix, i
     fp->row_step = row_step;
     fp->nloc = rt_tile_rows(npix, fp->width, row0, row_step) * fp->width;
     fp->log_pixel = -1;
-    fp->resume_min = ctx->resume_min;
+    fp->resume_min = ctx->resume_min >= 0 ? ctx->resume_min : use_wide(ctx) ? kResumeMinWide : kResumeMinBvh2;
     fp->step = ctx->step;
     fp->sun_skip = (ctx->sun_skip && env[3] == 0.0f && env[4] >= 0.0f && ctx->hs.colors_finite) ? 1 : 0;
     fp->sun_any = (ctx->sun_any && !ctx->hs.has_glass) ? 1 : 0;
@@ -769,7 +772,7 @@ int rt_set_option(rt_ctx* ctx, const char* key, int64_t value) {
         return RT_OK;
     }
     if (!std::strcmp(key, "resume_min")) {
-        if (value < 0 || value > 64) return set_err(ctx, RT_ERR_ARG, "resume_min must be in 0..64");
+        if (value < -1 || value > 64) return set_err(ctx, RT_ERR_ARG, "resume_min must be -1 (auto) or 0..64");
         ctx->resume_min = (int)value;
         return RT_OK;
     }

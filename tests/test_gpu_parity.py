@@ -260,10 +260,10 @@ def test_resumable_traversal_matches_plain_walk(kl, case):
     """resume_min (rays keep their traversal state across render-loop iterations) changes no hit."""
     sc, cam, env, npix, spp, mb, ibl = W.PARITY_CASES[case].inputs()
     frames = []
-    for t in (0, 1, 40, 64):
+    for t in (0, 1, 40, 48, 64, -1):
         kl.native.set_option("resume_min", t)
         frames.append(_launch(kl, sc, cam, env, npix, spp, mb, ibl, "fast"))
-    kl.native.set_option("resume_min", 40)
+    kl.native.set_option("resume_min", -1)
     for f in frames[1:]:
         np.testing.assert_array_equal(frames[0], f)
     with pytest.raises(_native.NativeError, match="resume_min"):

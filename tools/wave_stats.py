@@ -36,5 +36,5 @@ for name in names:
                "trav_cycle_share": round(c["cycles_trav"] / max(1, c["cycles_trav"] + c["cycles_shade"]), 4)}
         print(json.dumps(out), flush=True)
         for k in opts:   # back to the defaults for the next set
-            ctx.set_option(k, {"bvh_width": 0, "resume_min": 40}.get(k, 0))
+            ctx.set_option(k, {"bvh_width": 0, "resume_min": -1}.get(k, 0))
     ctx.close()
