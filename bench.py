@@ -121,8 +121,10 @@ def roofline(ctx, cnt: dict, kernel_ms: float, pixels: int, workload: str, share
     main, other, bound = (valu, hbm, "valu") if brute else (hbm, valu, "hbm")
     out = {"bound": bound}
     out.update(main)
-    if bound == "valu":   # the measured HBM traffic of the same kernel beside the VALU bound
-        out["traffic"], out["traffic_frac"] = hbm["traffic"], hbm["traffic_frac"]
+    # the measured HBM traffic of the same kernel (committed PMC summary) beside either bound; on the tree
+    # walk the algorithmic bytes are mostly served by the vL1D / L2, so `frac` is the SURVEY 8(d) byte
+    # rate against the HBM peak and `traffic_frac` what HBM actually moved
+    out["traffic"], out["traffic_frac"] = hbm["traffic"], hbm["traffic_frac"]
     out["kernel_ms"] = round(kernel_ms, 4)
     out["path"] = (f"brute force ({info['brute_boxes']} distinct leaf boxes, {info['brute_records']} triangles)"
                    if brute else f"SAH tree walk ({info['nodes']} nodes, {info['tris']} triangles)")
@@ -195,7 +197,8 @@ def time_config(ctx_factory, name: str, steps: int, warmup: int):
     ctx.close()
     return {"workload": wl.name, "value": round(npix * spp / dt / 1e6, 3), "unit": "Msamples/s",
             "ms_per_step": round(dt * 1e3, 3), "steps": steps, "warmup": warmup,
-            "roofline": {k: rf[k] for k in ("bound", "achieved", "peak", "unit", "frac", "kernel_ms", "path")},
+            "roofline": {k: rf.get(k) for k in ("bound", "achieved", "peak", "unit", "frac", "traffic", "traffic_frac",
+                                                "kernel_ms", "path", "profile")},
             "valu_frac": rf["frac"] if rf["bound"] == "valu" else rf["other_bound"]["frac"]}
 
 
