@@ -1694,6 +1694,10 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WIDE ?
             t_mid = clock64();
             if (lane == 0) c.cyc_shade += t_mid - t_iter;
         }
+        // lanes that finished their tile (DONE) take no part in the threshold: it is resume_min / 64
+        // of the lanes still rendering (all 64 until the pixel counters run dry)
+        const unsigned long long alive = __ballot(phase != DONE);
+        const int rthr = F.resume_min * __popcll(alive);
         while (true) {
             if (tracing && (WIDE ? (STEP ? wide_step<COUNT, OVF>(T, wnb, wlb, lst, c)
                                          : wide_round<COUNT, OVF>(T, wnb, wlb, lst, c))
@@ -1701,7 +1705,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WIDE ?
                                    : fast_round<COUNT, SMEM, OVF>(S, T, nb, tb, lst, kstride, c)))
                 tracing = false;
             const unsigned long long tr = __ballot(tracing);
-            if (tr == 0 || 64 - __popcll(tr) >= F.resume_min) break;
+            if (tr == 0 || 64 * __popcll(alive & ~tr) >= rthr) break;
         }
         if (COUNT && lane == 0) c.cyc_trav += clock64() - t_mid;
     }
