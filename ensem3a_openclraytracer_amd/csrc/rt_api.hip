@@ -26,10 +26,10 @@
 #include "rt_internal.h"
 
 #ifndef RT_RESUME_MIN_DEFAULT
-// FAST tree walk: resumable traversal threshold (rt_set_option "resume_min"; -1 = auto): 40 on the
-// BVH2 walk (C3 / C4 ms at 32 / 40 / 48: 157 / 150 / 151, 480 / 473 / 477), 48 on the 4-wide walk
-// (C5 at 40 / 48 / 52 / 56: 5,918 / 5,799 / 5,849 / 5,991)
-constexpr int kResumeMinBvh2 = 40, kResumeMinWide = 48;
+// FAST tree walk: resumable traversal threshold (rt_set_option "resume_min"; -1 = auto), out of 64
+// lanes still rendering: 36 on the BVH2 walk (C3 / C4 ms at 32 / 36 / 40: 138.8 / 136.8 / 136.5,
+// 446.8 / 452.6 / 455.0), 48 on the 4-wide walk (C5 at 40 / 48 / 52: 5,805 / 5,705 / 5,772)
+constexpr int kResumeMinBvh2 = 36, kResumeMinWide = 48;
 #endif
 #ifndef RT_BRUTE_MAX_DEFAULT
 #define RT_BRUTE_MAX_DEFAULT 64   // FAST tests every triangle of scenes up to this size (rt_set_option "brute_max")
