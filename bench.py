@@ -20,8 +20,11 @@ Extra fields (DESIGN.md 5 derives every number):
                      traversal, rt_count_work_detail) / the kernel's average
                      duration from HIP events on its stream; peak = the FP32 vector
                      issue rate (256 CUs x 4 SIMD x 32 lanes x 2.4 GHz).
-                   * tree walk (C3-C5): bound "hbm", achieved = SURVEY 8(d)
-                     algorithmic bytes per launch / kernel time, peak 8 TB/s.
+                   * tree walk (C3-C5): bound "cache", achieved = SURVEY 8(d)
+                     algorithmic bytes per launch / kernel time, peak = the
+                     L2 delivery rate incl. L1 reuse (36.9 TB/s, MI355X_MICROARCH.md):
+                     the walk's bytes are served by the vL1D / L2, not HBM;
+                     hbm_measured = PMC HBM bytes / kernel time vs 8 TB/s.
                    traffic = PMC-measured HBM bytes per launch (committed rocprofv3
                    summary in profiles/), issued = PMC-measured VALU lane slots
                    (SQ_INSTS_VALU x 64) per launch, when committed.
@@ -47,6 +50,7 @@ sys.path.insert(0, ROOT)
 
 METRIC = "Msamples/s Cornell box 1024x1024 64spp; 1/2/4/8-GPU scaling; HBM %peak"
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
+CACHE_PEAK_GBS = 36900.0       # L2 (all XCDs) delivery incl. L1 reuse, MI355X_MICROARCH.md "L2 (per XCD)"
 VALU_PEAK_TOPS = 78.6432       # 256 CUs x 4 SIMD x 32 lanes/clk x 2.4 GHz: VALU lane-ops/s (157.3 TFLOPS FP32 = 2 x this, FMA)
 
 # Algorithmic VALU lane-operations per unit of work ("VALU roofline"): IEEE basic
@@ -118,13 +122,18 @@ def roofline(ctx, cnt: dict, kernel_ms: float, pixels: int, workload: str, share
     hbm = {"achieved": round(byt / sec / 1e9, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
            "frac": round(byt / sec / 1e9 / HBM_PEAK_GBS, 4), "alg_bytes_per_launch": int(byt),
            "traffic": traffic, "traffic_frac": (round(traffic / sec / 1e9 / HBM_PEAK_GBS, 5) if traffic else None)}
-    main, other, bound = (valu, hbm, "valu") if brute else (hbm, valu, "hbm")
+    # tree walk: the algorithmic bytes are served by the vL1D / L2 (C3/C4 L1 hit rate ~90 %), so their
+    # rate is priced against the cache hierarchy's delivery ceiling, never against the HBM peak (it would
+    # exceed 1); what HBM actually moved is `hbm_measured` (PMC bytes of the same kernel)
+    cache = {"achieved": hbm["achieved"], "peak": CACHE_PEAK_GBS, "unit": "GB/s",
+             "frac": round(byt / sec / 1e9 / CACHE_PEAK_GBS, 4), "alg_bytes_per_launch": int(byt)}
+    main, other, bound = (valu, hbm, "valu") if brute else (cache, valu, "cache")
     out = {"bound": bound}
     out.update(main)
-    # the measured HBM traffic of the same kernel (committed PMC summary) beside either bound; on the tree
-    # walk the algorithmic bytes are mostly served by the vL1D / L2, so `frac` is the SURVEY 8(d) byte
-    # rate against the HBM peak and `traffic_frac` what HBM actually moved
     out["traffic"], out["traffic_frac"] = hbm["traffic"], hbm["traffic_frac"]
+    out["hbm_measured"] = {"achieved": (round(traffic / sec / 1e9, 2) if traffic else None), "peak": HBM_PEAK_GBS,
+                           "unit": "GB/s", "frac": hbm["traffic_frac"],
+                           "what": "PMC HBM bytes (2 x FETCH_SIZE + WRITE_SIZE, gfx950 correction) / kernel time"}
     out["kernel_ms"] = round(kernel_ms, 4)
     out["path"] = (f"brute force ({info['brute_boxes']} distinct leaf boxes, {info['brute_records']} triangles)"
                    if brute else f"SAH tree walk ({info['nodes']} nodes, {info['tris']} triangles)")
@@ -198,7 +207,7 @@ def time_config(ctx_factory, name: str, steps: int, warmup: int):
     return {"workload": wl.name, "value": round(npix * spp / dt / 1e6, 3), "unit": "Msamples/s",
             "ms_per_step": round(dt * 1e3, 3), "steps": steps, "warmup": warmup,
             "roofline": {k: rf.get(k) for k in ("bound", "achieved", "peak", "unit", "frac", "traffic", "traffic_frac",
-                                                "kernel_ms", "path", "profile")},
+                                                "hbm_measured", "kernel_ms", "path", "profile")},
             "valu_frac": rf["frac"] if rf["bound"] == "valu" else rf["other_bound"]["frac"]}
 
 
