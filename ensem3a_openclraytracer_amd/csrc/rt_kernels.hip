@@ -381,6 +381,12 @@ constexpr int BRUTE_WAVE_LDS = 64 * 6 * 4 + 64 * 8 + 256 * 4;   // ray table | b
 // wave's LDS instructions in order; this keeps the compiler from reordering them
 // across the hand-off (it would otherwise move a lane's read of another lane's
 // entry above the write it depends on).
+// base + the number of bits of mask m below this lane (v_mbcnt_lo / v_mbcnt_hi: two VALU, no lane-mask
+// registers)
+__device__ __forceinline__ unsigned lane_prefix(unsigned long long m, unsigned base) {
+    return __builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, base));
+}
+
 __device__ __forceinline__ void wave_lds_sync() {
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -398,7 +404,7 @@ __device__ Hit trace_brute_compact(const DevScene& S, rtm_f3 o, rtm_f3 d, char* 
     if (COUNT && sub == 0) c.rays++;
     const unsigned long long act = __ballot(1);
     const int nact = __popcll(act);
-    const int myrank = __popcll(act & ((1ull << lane) - 1ull));
+    const int myrank = (int)lane_prefix(act, 0u);
     float* ray = reinterpret_cast<float*>(wl);                                   // [6][64]
     unsigned long long* bestk = reinterpret_cast<unsigned long long*>(wl + 64 * 6 * 4);
     unsigned* ring = reinterpret_cast<unsigned*>(wl + 64 * 6 * 4 + 64 * 8);   // owner << 16 | triangle
@@ -445,7 +451,7 @@ __device__ Hit trace_brute_compact(const DevScene& S, rtm_f3 o, rtm_f3 d, char* 
         const unsigned n = (unsigned)__popcll(m);
         if (pass) {
             if (COUNT) c.tris += qb >= 0 ? 2 : 1;
-            const unsigned r = tail + (unsigned)__popcll(m & ((1ull << lane) - 1ull));
+            const unsigned r = lane_prefix(m, tail);
             ring[r & 255] = (tl << 16) | qa;
             if (qb >= 0) ring[(r + n) & 255] = (tl << 16) | (unsigned)qb;
         }
