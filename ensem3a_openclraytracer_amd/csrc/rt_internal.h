@@ -14,7 +14,10 @@ constexpr int kStackLds = 20;
 constexpr int kStackLdsWide = 11;
 constexpr int kNodeF4 = 4;             // float4 per FAST BVH2 node (DevScene::nodes)
 constexpr int kMaxLanesPerCu = 2048;   // resident threads per CU (gfx950)
-constexpr int kBoxGroup = 4;           // leaf boxes per scalar load group of the brute-force loop (DevScene::brute_box)
+#ifndef RT_BOX_GROUP
+#define RT_BOX_GROUP 4
+#endif
+constexpr int kBoxGroup = RT_BOX_GROUP;  // leaf boxes per scalar load group of the brute-force loop (DevScene::brute_box)
 constexpr int kMatF = 8;               // floats per device material row (DevScene::mat)
 // FAST tree walk over the 4-wide layout when the BVH2 node array exceeds this (option "bvh_width"
 // 0 = auto): trees that do not fit the L2, where the walk is bound by the latency of dependent
