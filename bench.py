@@ -97,9 +97,10 @@ def valu_ops(cnt: dict, pixels: int) -> float:
 
 
 def alg_bytes(cnt: dict, wb: dict, pixels: int) -> float:
-    # 32 B per box tested (a FAST node = 64 B: both children), 36 B per triangle test,
-    # 40 B per ray hit record, 16 B per IBL lookup, + the tile written (12 B per pixel)
-    return (cnt["node_fetches"] * wb["node_fetch"] + cnt["tri_tests"] * wb["tri_test"] + cnt["rays"] * wb["ray"]
+    # 32 B per box tested (a BVH2 node tests 2, a 4-wide node up to 4, a wide leaf its
+    # exact box), 36 B per triangle test, 40 B per ray hit record, 16 B per IBL lookup, + the tile
+    # written (12 B per pixel)
+    return (cnt["box_tests"] * wb["box_test"] + cnt["tri_tests"] * wb["tri_test"] + cnt["rays"] * wb["ray"]
             + cnt["env_lookups"] * wb["env_lookup"] + pixels * 12.0)
 
 

@@ -27,7 +27,7 @@ EXPORTED = (
     "rt_render", "rt_render_device", "rt_tile_rows", "rt_count_work", "rt_count_work_detail", "rt_work_bytes", "rt_gamma",
     "rt_render_rgb8", "rt_rgb8_device", "rt_rgb8",
     "rt_bvh_build", "rt_device_count", "rt_debug_math", "rt_debug_trace", "rt_debug_scene_info", "rt_debug_pixel_log",
-    "rt_debug_wave_counts",
+    "rt_debug_wave_counts", "rt_debug_quantise_axis",
     "rt_obj_parse", "rt_obj_size", "rt_obj_copy", "rt_obj_free", "rt_obj_last_error",
 )
 
@@ -227,7 +227,7 @@ class Context:
     def work_bytes(self):
         out = np.zeros(4, dtype=np.float64)
         self._check(lib().rt_work_bytes(self.handle, out.ctypes.data))
-        return dict(zip(("node_fetch", "tri_test", "ray", "env_lookup"), map(float, out)))
+        return dict(zip(("box_test", "tri_test", "ray", "env_lookup"), map(float, out)))
 
     def gamma(self, src, out=None):
         s = f32(src)

@@ -25,12 +25,10 @@
 #include "bvh_sah.h"
 #include "rt_internal.h"
 
-#ifndef RT_RESUME_MIN_DEFAULT
 // FAST tree walk: resumable traversal threshold (rt_set_option "resume_min"; -1 = auto), out of 64
 // lanes still rendering: 36 on the BVH2 walk (C3 / C4 ms at 32 / 36 / 40: 138.8 / 136.8 / 136.5,
 // 446.8 / 452.6 / 455.0), 48 on the 4-wide walk (C5 at 40 / 48 / 52: 5,805 / 5,705 / 5,772)
 constexpr int kResumeMinBvh2 = 36, kResumeMinWide = 48;
-#endif
 #ifndef RT_BRUTE_MAX_DEFAULT
 #define RT_BRUTE_MAX_DEFAULT 64   // FAST tests every triangle of scenes up to this size (rt_set_option "brute_max")
 #endif
@@ -176,12 +174,21 @@ inline bool fidx(float v, int64_t limit, int32_t* out) {
 // kernels dequantise it (rt_kernels.hip wide_step; this file is built with -ffp-contract=off).
 inline float deq(float p, uint32_t q, float s) { return p + (float)q * s; }
 
+}  // namespace
+
 // Per-axis quantisation of up to 4 child boxes against their union's lower corner p: a scale
 // 2^e and byte bounds whose dequantised box contains each child's exact box.  Returns the
-// biased exponent byte (scale = as_float(e << 23)).
-uint32_t quantise_axis(float p, const float* lo, const float* hi, int n, uint8_t* qlo, uint8_t* qhi) {
+// biased exponent byte (scale = as_float(e << 23)), or -1 when no exponent up to 2^100 gives
+// containing bounds (non-finite bounds, or an extent beyond 255 * 2^100): the caller must then not
+// use the quantised layout (a dequantised box that is not a superset could cull a hit subtree).
+extern "C" int rt_debug_quantise_axis(float p, const float* lo, const float* hi, int n, uint8_t* qlo, uint8_t* qhi) {
+    if (n < 1 || n > 4 || !lo || !hi || !qlo || !qhi) return -1;
+    if (!std::isfinite(p)) return -1;
     double ext = 0.0;
-    for (int c = 0; c < n; ++c) ext = std::max(ext, (double)hi[c] - (double)p);
+    for (int c = 0; c < n; ++c) {
+        if (!std::isfinite(lo[c]) || !std::isfinite(hi[c])) return -1;
+        ext = std::max(ext, (double)hi[c] - (double)p);
+    }
     int e = ext > 0.0 ? (int)std::ceil(std::log2(ext / 255.0)) : -100;
     e = std::min(std::max(e, -100), 100);
     for (;; ++e) {
@@ -197,9 +204,12 @@ uint32_t quantise_axis(float p, const float* lo, const float* hi, int n, uint8_t
             qlo[c] = (uint8_t)a;
             qhi[c] = (uint8_t)b;
         }
-        if (ok || e >= 100) return (uint32_t)(e + 127);
+        if (ok) return e + 127;
+        if (e >= 100) return -1;
     }
 }
+
+namespace {
 
 // Wide layout of the FAST tree (DevScene::wnodes / wleaves, option "bvh_width" 4): the binary tree
 // collapsed to nodes of up to 4 children (the internal child with the largest surface area is
@@ -283,7 +293,18 @@ void emit_wide(HostScene& hs, const int32_t* L, const int32_t* R, const int32_t*
         }
         uint8_t ql[3][4] = {}, qh[3][4] = {};
         uint32_t meta = 0;
-        for (int a = 0; a < 3; ++a) meta |= quantise_axis(p[a], lo[a], hi[a], n, ql[a], qh[a]) << (8 * a);
+        for (int a = 0; a < 3; ++a) {
+            const int ex = rt_debug_quantise_axis(p[a], lo[a], hi[a], n, ql[a], qh[a]);
+            if (ex < 0) {   // no containing quantisation: no wide layout (use_wide() keeps the BVH2 walk)
+                hs.wnodes.clear();
+                hs.wleaves.clear();
+                hs.nwnodes = 0;
+                hs.wroot_ref = 0;
+                hs.wdepth = 1;
+                return;
+            }
+            meta |= (uint32_t)ex << (8 * a);
+        }
         o[0] = p[0]; o[1] = p[1]; o[2] = p[2]; o[3] = as_f32((int32_t)meta);
         for (int c = 0; c < 4; ++c)
             o[4 + c] = as_f32(c < n ? (is_inner(ch[c]) ? wide_of[ch[c]] : leaf_ref(ch[c])) : INT32_MIN);
@@ -758,6 +779,8 @@ int rt_set_option(rt_ctx* ctx, const char* key, int64_t value) {
         for (auto& d : ctx->devs) {
             HIP_OR_RET(ctx, hipSetDevice(d.id));
             HIP_OR_RET(ctx, order_after_last(d, d.stream));
+            // a launch in flight on another stream may still read the buffers upload() can free
+            HIP_OR_RET(ctx, hipStreamSynchronize(d.stream));
             HIP_OR_RET(ctx, upload(d.nodes, hs.nodes, d.stream));
             HIP_OR_RET(ctx, upload(d.wnodes, hs.wnodes, d.stream));
             HIP_OR_RET(ctx, upload(d.wleaves, hs.wleaves, d.stream));
@@ -929,6 +952,8 @@ int rt_set_scene(rt_ctx* ctx, const float* vp, int64_t nvp, const float* vn, int
     for (auto& d : ctx->devs) {
         HIP_OR_RET(ctx, hipSetDevice(d.id));
         HIP_OR_RET(ctx, order_after_last(d, d.stream));
+        // a launch in flight on another stream may still read the buffers upload() / ensure() free
+        HIP_OR_RET(ctx, hipStreamSynchronize(d.stream));
         HIP_OR_RET(ctx, upload(d.nodes, hs.nodes, d.stream));
         HIP_OR_RET(ctx, upload(d.wnodes, hs.wnodes, d.stream));
         HIP_OR_RET(ctx, upload(d.wleaves, hs.wleaves, d.stream));
@@ -997,8 +1022,12 @@ hipError_t setup_pilot(rt_ctx* ctx, Device& d, rt::FrameParams& fp) {
     const size_t n = (size_t)fp.nloc;
     // state 32 B | cost 4 B | order 4 B per pixel, bin totals + offsets (2 x 256), the chunk costs +
     // chunk order (at most one chunk per pixel) and the sort's segment histograms (256 per 256 chunks)
-    hipError_t e = ensure(d.pilot, n * 40 + 2 * 256 * sizeof(uint32_t) + 2 * (n + 1) * sizeof(uint32_t) +
-                                       (n + 256) * sizeof(uint32_t));
+    const size_t need = n * 40 + 2 * 256 * sizeof(uint32_t) + 2 * (n + 1) * sizeof(uint32_t) +
+                        (n + 256) * sizeof(uint32_t);
+    hipError_t e = hipSuccess;
+    // growing frees the old buffer from the host: the last launch (any stream) may still use it
+    if (d.pilot.bytes < need && d.pending) e = hipEventSynchronize(d.done);
+    if (e == hipSuccess) e = ensure(d.pilot, need);
     if (e != hipSuccess) return e;
     char* base = (char*)d.pilot.p;
     fp.pilot = k;
@@ -1187,8 +1216,10 @@ int rt_work_bytes(rt_ctx* ctx, double out[4]) {
     // Algorithmic bytes per unit: 32 B per box test (24 B AABB + 8 B child/leaf
     // refs), 36 B per triangle test (v0, e1, e2), 40 B per hit record, 16 B per IBL lookup.
     if (!ctx || !out) return set_err(ctx, RT_ERR_ARG, "null argument");
-    out[0] = effective_traversal(ctx) == RT_TRAVERSAL_FAST ? 64.0  // a FAST node tests both child boxes
-                                                            : 32.0;                // one reference node = one box
+    // out[0] prices counts[9] (box tests) of rt_count_work_detail: a BVH2 node tests 2 child boxes, a
+    // 4-wide node up to 4, a wide leaf its exact box again, a REF node 1 -- so every layout is priced
+    // per box actually tested
+    out[0] = 32.0;
     out[1] = 36.0;
     out[2] = 40.0;
     out[3] = 16.0;

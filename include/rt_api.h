@@ -130,9 +130,10 @@ int rt_count_work_detail(rt_ctx* ctx, const float cam[10], const float env[5], i
                          int max_bounce, int row0, int row_step, uint64_t counts[16]);
 
 /* Algorithmic bytes per unit of the counters above:
- * out[0] = per node fetch (32 B per box tested: 64 for a FAST node, which
- * tests both children; 32 for a REF node), out[1] = 36 per triangle test,
- * out[2] = 40 per ray hit record, out[3] = 16 per environment lookup. */
+ * out[0] = 32 B per ray-box slab test (counts[9] of rt_count_work_detail:
+ * a BVH2 node tests 2 child boxes, a 4-wide node up to 4, a wide leaf its
+ * exact box, a REF node 1), out[1] = 36 per triangle test, out[2] = 40 per
+ * ray hit record, out[3] = 16 per environment lookup. */
 int rt_work_bytes(rt_ctx* ctx, double out[4]);
 
 /* Gamma kernel of ImgProcessing.cl:1-10: out[k] = powr(min(in[k],1), 2.2)

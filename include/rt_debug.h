@@ -42,6 +42,13 @@ int rt_debug_wave_counts(rt_ctx* ctx, const float cam[10], const float env[5], i
  * brute-force path, out[6], out[7] = 0. */
 int rt_debug_scene_info(rt_ctx* ctx, int64_t out[8]);
 
+/* Host-only (no device): the per-axis quantisation of the 4-wide layout (rt_api.hip emit_wide).
+ * For up to n = 4 child intervals [lo[c], hi[c]] against the lower corner p, returns the biased
+ * exponent byte e (scale 2^(e-127)) and byte bounds with p + qlo[c] * 2^(e-127) <= lo[c] and
+ * p + qhi[c] * 2^(e-127) >= hi[c] in fp32, or -1 when no scale up to 2^100 contains every interval
+ * (non-finite bounds, extents beyond 255 * 2^100): the scene then keeps the BVH2 walk. */
+int rt_debug_quantise_axis(float p, const float* lo, const float* hi, int n, uint8_t* qlo, uint8_t* qhi);
+
 #ifdef __cplusplus
 }
 #endif

@@ -12,7 +12,7 @@ class _Ctx:
                 "nodes": 7255, "tris": 7256}
 
     def work_bytes(self):
-        return {"node_fetch": 64.0, "tri_test": 36.0, "ray": 40.0, "env_lookup": 16.0}
+        return {"box_test": 32.0, "tri_test": 36.0, "ray": 40.0, "env_lookup": 16.0}
 
 
 def _counts(per_sample, samples):

@@ -81,13 +81,17 @@ def test_launches_on_two_streams_do_not_race(case):
     ctx.close()
 
 
-def test_scene_upload_waits_for_a_launch_in_flight():
+@pytest.mark.parametrize("first,second,size", [
+    ("monkey_c3_64_s4", "cornell_64_s4", (512, 512, 64)),     # smaller scene: buffers reused
+    ("cornell_64_s4", "monkey_c3_64_s4", (1024, 1024, 256)),  # larger scene: buffers freed + reallocated
+])
+def test_scene_upload_waits_for_a_launch_in_flight(first, second, size):
     """rt_set_scene right after an asynchronous launch on a caller's stream: the launch still
-    renders the old scene (the upload is ordered after it)."""
+    renders the old scene (the upload, and any free of a buffer it reads, is ordered after it)."""
     import torch
-    ctx, cam, env, npix, spp, mb = _ctx("monkey_c3_64_s4", (512, 512, 64))   # ~10 ms in flight
+    ctx, cam, env, npix, spp, mb = _ctx(first, size)   # ~10-30 ms in flight
     want = ctx.render(cam, env, npix, spp, mb)
-    sc2, *_ = W.PARITY_CASES["cornell_64_s4"].inputs()
+    sc2, *_ = W.PARITY_CASES[second].inputs()
     s = torch.cuda.Stream()
     a = torch.empty(3 * npix, dtype=torch.float32, device="cuda")
     ctx.render_device(cam, env, npix, spp, mb, 0, 1, a.data_ptr(), s.cuda_stream)

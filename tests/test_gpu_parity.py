@@ -520,7 +520,8 @@ def test_full_c2_every_pixel_vs_oracle(kl):
     f = _launch(kl, sc, cam, env, npix, spp, mb, ibl, "fast")
     st = compare.assert_gate(f, ora, "C2 full frame, fast vs oracle")
     bad = np.unique(np.nonzero(f != ora)[0] // 3)
-    assert bad.size <= 8, bad[:20]
+    # pinned to the measured set: any new divergent pixel fails and has to be explained
+    assert set(bad.tolist()) <= {203399}, bad[:20]
 
 
 @pytest.mark.parametrize("row_step", [8, 16])
