@@ -30,7 +30,8 @@ Extra fields (DESIGN.md 5 derives every number):
                    (SQ_INSTS_VALU x 64) per launch, when committed.
   host_boundary -- rt_render (launch_Raytracing's blocking C-ABI: kernel + copy of
                    the frame into caller memory), timed over the same W/K steps.
-  configs       -- N=1 only: C3 and C4 timed the same way (2 steps, 1 warmup).
+  configs       -- N=1 only: C3 and C4 timed the same way (2 steps, 1 warmup), C5 (1 step, 1
+                   warmup: 5-6 s per frame).
   cpu_baseline  -- the CPU oracle (a C restatement of the reference kernel, OpenMP)
                    timed on this host on a bounded row sample of the same frame.
 """
@@ -180,7 +181,7 @@ def cpu_baseline(wl, scene, ibl, cam, env, target_s: float = 10.0):
 
 
 def time_config(ctx_factory, name: str, steps: int, warmup: int):
-    """One-GPU device-resident timing of another BASELINE config (C3/C4), same method as the headline."""
+    """One-GPU device-resident timing of another BASELINE config (C3/C4/C5), same method as the headline."""
     import torch
     from ensem3a_openclraytracer_amd import workloads as Wk
     wl = Wk.CONFIGS[name]
@@ -416,6 +417,7 @@ def main():
             ctx.close()
             ctx = None
             line["configs"] = {c: time_config(make_ctx, c, 2, 1) for c in ("C3", "C4")}
+            line["configs"]["C5"] = time_config(make_ctx, "C5", 1, 1)
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(wl, scene, ibl, cam, env)
         print(json.dumps(line), flush=True)

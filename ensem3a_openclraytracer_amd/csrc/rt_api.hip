@@ -95,6 +95,7 @@ struct rt_ctx {
     int brute_max = RT_BRUTE_MAX_DEFAULT;
     int resume_min = -1;
     int team = 0;  // brute-force lanes per pixel, 0 = auto
+    int walk_team = 0;  // tree walk (BVH2 item steps): lanes per pixel walking each ray together, 0 = auto
     int max_waves = 0;  // persistent grid cap in waves per SIMD, 0 = occupancy limit
     int step = 0;       // tree-walk traversal loop: 0 auto, 1 one item per step, 2 descend-until-leaf rounds
     int sun_skip = 1;   // FAST: do not trace shadow rays of an unlit sun (FrameParams::sun_skip)
@@ -685,6 +686,7 @@ int check_frame(rt_ctx* ctx, const float* cam, const float* env, int64_t npix, i
     fp->pilot_cost = nullptr;
     fp->pilot_order = nullptr;
     fp->team = ctx->team;
+    fp->walk_team = ctx->walk_team;
     fp->max_waves = ctx->max_waves;
     fp->log_buf = nullptr;
     fp->log_cap = 0;
@@ -803,6 +805,12 @@ int rt_set_option(rt_ctx* ctx, const char* key, int64_t value) {
         if (value != 0 && value != 1 && value != 2 && value != 4 && value != 8)
             return set_err(ctx, RT_ERR_ARG, "team must be 0 (auto), 1, 2, 4 or 8");
         ctx->team = (int)value;
+        return RT_OK;
+    }
+    if (!std::strcmp(key, "walk_team")) {
+        if (value != 0 && value != 1 && value != 2 && value != 4)
+            return set_err(ctx, RT_ERR_ARG, "walk_team must be 0 (auto), 1, 2 or 4");
+        ctx->walk_team = (int)value;
         return RT_OK;
     }
     if (!std::strcmp(key, "sun_any")) {

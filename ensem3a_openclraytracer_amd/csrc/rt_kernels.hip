@@ -227,6 +227,14 @@ struct LaneStack {
         else e = ovf[slot(off)];
         return e;
     }
+    // entry `off` of the stack of the lane dl lanes away in the same wave (team walk steals)
+    template <bool OVF>
+    __device__ __forceinline__ int2 get_lane(unsigned off, int dl) const {
+        int2 e;
+        if (!OVF || off < cap) e = *reinterpret_cast<const int2*>(lds + off + 8 * dl);
+        else e = ovf[(unsigned)((int)slot(off) + dl)];
+        return e;
+    }
 };
 
 __device__ __forceinline__ LaneStack lane_stack(const DevScene& S, int* lds_base) {
@@ -1283,6 +1291,117 @@ __device__ __forceinline__ bool fast_step(const DevScene& S, FastRay& R, const c
     return true;
 }
 
+// ---- team traversal: TS lanes walk one ray (tiles with about one pixel per lane, option "walk_team") ----
+// When a tile has no more pixels than the device has lanes, a frame lasts as long as its slowest
+// pixel's chain of samples, and a chain advances one dependent node fetch per step.
+// Here TS consecutive lanes (a team, TS = 2 or 4, inside one DPP quad) carry the same pixel with
+// identical shading arithmetic and split each ray's tree walk: every lane runs trace_fast's
+// closest-first descent on its own LDS stack, and a lane whose stack runs dry steals the BOTTOM
+// entry (the shallowest: the largest untested subtree) of a teammate's stack.  A lane's stack top
+// evolves exactly as in a one-lane walk started at the subtree it took, so it never holds more than
+// DevScene::depth entries; steals only remove entries from the bottom.  The team's best hit (k, rank,
+// triangle) is reduced across the team (DPP within the quad) in every step where a lane improved it,
+// so culling uses the team's best.  The hit is the minimum (k, rank) over accepted triangles, which
+// no traversal order changes (every ancestor box is a union of leaf boxes): the frame is the one-lane
+// walk's, bit for bit.
+constexpr int NO_ITEM = INT_MIN;
+
+template <int M>
+__device__ __forceinline__ int quad_xor(int x) {   // lane ^ M within the quad (M = 1, 2): one DPP move
+    return __builtin_amdgcn_update_dpp(0, x, M == 1 ? 0xB1 : 0x4E, 0xF, 0xF, false);
+}
+
+// the r-th set bit (r < popcount) of a mask of at most 4 bits (team masks, shifted to bit 0)
+__device__ __forceinline__ int nth_bit4(unsigned m, unsigned r) {
+    for (unsigned k = 0; k < r; ++k) m &= m - 1u;
+    return __builtin_ctz(m);
+}
+
+// One step of a team's walk over the BVH2 item layout (fast_step's loads and arithmetic).  R.item is
+// the lane's own item (NO_ITEM: none), R.soff its stack top and boff its stack bottom (bytes).
+// Returns true (for every lane of the team) when the team's ray is finished.
+template <int TS, bool COUNT, bool SOA, bool OVF>
+__device__ __forceinline__ bool team_step(FastRay& R, unsigned& boff, const char* nb, const char* tb,
+                                          const LaneStack& st, unsigned kstride, Cnt& c) {
+    const unsigned lane = threadIdx.x & 63u;
+    const unsigned tbase = lane & ~(unsigned)(TS - 1);
+    const unsigned sub = lane - tbase;
+    // 1. a lane without an item pops its own stack (entries behind the team's best are discarded)
+    if (R.item == NO_ITEM) {
+        while (R.soff > boff) {
+            R.soff -= st.stride;
+            const int2 en = st.template get<OVF>(R.soff);
+            if (__int_as_float(en.y) <= R.bk * CULL_MARGIN) {
+                R.item = en.x;
+                break;
+            }
+        }
+        if (R.soff == boff) R.soff = boff = 0u;   // drained: the next subtree starts a fresh stack
+    }
+    // 2. lanes still without an item steal the bottom entry of teammates with a non-empty stack
+    const unsigned idle = (unsigned)(__ballot(R.item == NO_ITEM) >> tbase) & ((1u << TS) - 1u);
+    const unsigned vict = (unsigned)(__ballot(R.soff > boff) >> tbase) & ((1u << TS) - 1u);
+    if (idle && vict) {
+        const unsigned nth = (unsigned)__popc(idle), nv = (unsigned)__popc(vict);
+        const unsigned below = (1u << sub) - 1u;
+        const bool thief = ((idle >> sub) & 1u) && (unsigned)__popc(idle & below) < nv;
+        const bool robbed = ((vict >> sub) & 1u) && (unsigned)__popc(vict & below) < nth;
+        const int v = thief ? (int)tbase + nth_bit4(vict, (unsigned)__popc(idle & below)) : (int)lane;
+        const unsigned vb = (unsigned)__shfl((int)boff, v, 64);
+        if (thief) {
+            const int2 en = st.template get_lane<OVF>(vb, v - (int)lane);
+            if (__int_as_float(en.y) <= R.bk * CULL_MARGIN) R.item = en.x;
+        }
+        if (robbed) boff += st.stride;
+    }
+    // 3. every lane with an item processes it (fast_step)
+    bool improved = false;
+    if (R.item != NO_ITEM) {
+        const bool node = R.item >= 0;
+        const char* p = node ? nb + (SOA ? 16u : 16u * kNodeF4) * (unsigned)R.item : tb + ~(unsigned)R.item;
+        const unsigned ks = node ? kstride : 16u;
+        const float4 g0 = *reinterpret_cast<const float4*>(p);
+        const float4 g1 = *reinterpret_cast<const float4*>(p + ks);
+        const float4 g2 = *reinterpret_cast<const float4*>(p + 2 * ks);
+        const int2 e = *reinterpret_cast<const int2*>(p + (node ? 3 * ks : 0u));
+        if (node) {
+            if (COUNT) { c.nodes++; c.boxes += 2; }
+            R.item = node_pick<OVF>(g0, g1, g2, e, R.o, R.ix, R.iy, R.iz, R.bk * CULL_MARGIN, st, R.soff);
+        } else {
+            if (COUNT) c.tris++;
+            float k;
+            int rank;
+            if (mt_vals(g0, g1, g2, R.o, R.d, &k, &rank) && k > 0.0001f &&
+                (k < R.bk || (k == R.bk && rank < R.brank))) {
+                R.bk = k;
+                R.bt = 48 * __float_as_int(g1.w);
+                R.brank = rank;
+                improved = true;
+            }
+            R.item = NO_ITEM;
+        }
+    }
+    if (COUNT) count_wave(c.wave_trav);
+    // 4. the team's best: lowest (k, rank) over the team, in every lane
+    if (__ballot(improved)) {
+#pragma unroll
+        for (int m = 1; m < TS; m <<= 1) {
+            const float ok = __int_as_float(m == 1 ? quad_xor<1>(__float_as_int(R.bk)) : quad_xor<2>(__float_as_int(R.bk)));
+            const int orank = m == 1 ? quad_xor<1>(R.brank) : quad_xor<2>(R.brank);
+            const int obt = m == 1 ? quad_xor<1>(R.bt) : quad_xor<2>(R.bt);
+            if (ok < R.bk || (ok == R.bk && orank < R.brank)) {
+                R.bk = ok;
+                R.brank = orank;
+                R.bt = obt;
+            }
+        }
+        if (R.any && R.bt >= 0) return true;   // a shadow ray's hit only matters as hit / miss
+    }
+    // 5. finished when no lane of the team holds an item or a stack entry
+    const unsigned busy = (unsigned)(__ballot(R.item != NO_ITEM || R.soff > boff) >> tbase) & ((1u << TS) - 1u);
+    return busy == 0u;
+}
+
 // One item of the walk over the 4-wide quantised layout (DevScene::wnodes, rt_api.hip emit_wide):
 // an internal node -- its up to 4 child boxes dequantised (p + q * 2^e per bound) and tested, the
 // hit children sorted by entry distance, the nearest continued and the others pushed farthest first
@@ -1431,7 +1550,8 @@ constexpr size_t kStepMaxBytes = 16u << 20;
 // BVH2 walk (C3/C4) is bound by the vector memory pipeline and keeps 4 waves with its whole 20-entry
 // stack in LDS (5 waves with a 14-entry spilling stack: C3 149 -> 157 ms, C4 475 -> 502 ms).
 constexpr int kWideWaves = 7;
-template <bool COUNT, bool LOG, bool SMEM, bool OVF, bool STEP, bool WIDE>
+// TS > 1: teams of TS lanes per pixel walk each ray together (team_step; BVH2 item steps only).
+template <bool COUNT, bool LOG, bool SMEM, bool OVF, bool STEP, bool WIDE, int TS = 1>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WIDE ? kWideWaves : 4))) render_resume_kernel(DevScene S, FrameParams F, float* __restrict__ out,
                                                       unsigned long long* __restrict__ counts,
                                                       unsigned int* __restrict__ work_counter,
@@ -1464,6 +1584,11 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WIDE ?
     const int spp = F.spp, maxB = F.max_bounce;
     const unsigned int nloc = (unsigned int)F.nloc;
     const int lane = threadIdx.x & 63;
+    static_assert(TS == 1 || (TS == 2 || TS == 4) && STEP && !WIDE, "team walk: BVH2 item steps, 2 or 4 lanes");
+    const int team_lane0 = lane & ~(TS - 1);
+    const bool team_leader = lane == team_lane0;
+    const unsigned long long team_leaders = TS == 1 ? ~0ull : TS == 2 ? 0x5555555555555555ull : 0x1111111111111111ull;
+    unsigned boff = 0;   // team walk: bottom of this lane's stack (bytes; entries below were stolen)
 
     int phase = FETCH;
     bool tracing = false;
@@ -1488,11 +1613,12 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WIDE ?
     int cost = 0;        // pass 1: rays this pixel traced (pilot_cost)
 
     auto write_pixel = [&]() __attribute__((always_inline)) {
-        store_pixel(out, p, acc, spp);
+        if (team_leader) store_pixel(out, p, acc, spp);
     };
     // pass 1 (FrameParams::pass): after the pilot samples, save the pixel's state for pass 2; the
     // pixel is written (and its cost set to 0) when all its samples are done
     auto save_pilot = [&]() __attribute__((always_inline)) {
+        if (!team_leader) return;
         F.pilot_state[2 * (int64_t)p] = make_float4(acc.x, acc.y, acc.z, kc);
         F.pilot_state[2 * (int64_t)p + 1] =
             make_float4(__uint_as_float(seed0), __uint_as_float(seed1), __int_as_float(tc), __int_as_float(s));
@@ -1528,15 +1654,19 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WIDE ?
         ++cost;
         tracing = !fast_init<COUNT>(S, T, o, d, c);
         if (WIDE) T.item = S.wroot_ref;
+        if (TS > 1) {   // the team's first lane takes the root; the others steal from it
+            if (!team_leader) T.item = NO_ITEM;
+            boff = 0;
+        }
         T.any = false;
     };
 
     while (true) {
         const unsigned long long t_iter = COUNT ? clock64() : 0;
-        // -- refill: ballot the lanes that need a pixel, one atomic per wave --
-        const unsigned long long need = __ballot(phase == FETCH);
+        // -- refill: ballot the lanes that need a pixel, one atomic per wave (one pixel per team) --
+        const unsigned long long need = __ballot(phase == FETCH) & team_leaders;
         if (need) {
-            const unsigned int q = take_pixel(pq, need, lane, work_counter, nloc, lane);
+            const unsigned int q = take_pixel(pq, need, team_lane0, work_counter, nloc, lane);
             if (phase == FETCH) {
                 bool ok = q < nloc;
                 if (ok) {
@@ -1705,8 +1835,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WIDE ?
         const unsigned long long alive = __ballot(phase != DONE);
         const int rthr = F.resume_min * __popcll(alive);
         while (true) {
-            if (tracing && (WIDE ? (STEP ? wide_step<COUNT, OVF>(T, wnb, wlb, lst, c)
-                                         : wide_round<COUNT, OVF>(T, wnb, wlb, lst, c))
+            if (tracing && (TS > 1 ? team_step<TS, COUNT, SMEM, OVF>(T, boff, nb, tb, lst, kstride, c)
+                            : WIDE ? (STEP ? wide_step<COUNT, OVF>(T, wnb, wlb, lst, c)
+                                           : wide_round<COUNT, OVF>(T, wnb, wlb, lst, c))
                             : STEP ? fast_step<COUNT, SMEM, OVF>(S, T, nb, tb, lst, kstride, c)
                                    : fast_round<COUNT, SMEM, OVF>(S, T, nb, tb, lst, kstride, c)))
                 tracing = false;
@@ -1716,6 +1847,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WIDE ?
         if (COUNT && lane == 0) c.cyc_trav += clock64() - t_mid;
     }
     if (COUNT) {
+        if (!team_leader) {   // a team's lanes repeat its pixel's shading and rays: counted once
+            c.rays = 0; c.env = 0; c.diffuse = 0; c.glossy = 0; c.glass = 0; c.sun = 0; c.samples = 0;
+        }
         unsigned long long v[NCOUNTS] = {c.nodes, c.tris, c.rays, c.env, c.dropped, c.wave_trav, c.wave_outer,
                                           c.cyc_shade, c.cyc_trav, c.boxes, c.diffuse, c.glossy, c.glass,
                                           c.sun, c.samples};
@@ -1762,6 +1896,14 @@ __global__ void rgb8_kernel(const float* __restrict__ in, uint8_t* __restrict__ 
     }
 }
 
+// FrameParams::walk_team = 0 (auto): lanes per pixel of the tree walk from the tile's pixels per
+// resident lane (provisional: one lane per pixel until measured)
+inline int auto_walk_team(int64_t nloc, int64_t lanes) {
+    (void)nloc;
+    (void)lanes;
+    return 1;
+}
+
 template <int TRAV, bool COUNT, bool LOG, bool SMEM = false, bool RESUME = false, bool OVF = false,
           bool BRUTE = false, bool STEP = true, bool WIDE = false>
 hipError_t launch_t(const DevScene& sc, const FrameParams& fp, int block, float* d_out, unsigned long long* d_counts,
@@ -1786,6 +1928,14 @@ hipError_t launch_t(const DevScene& sc, const FrameParams& fp, int block, float*
     // blocks per CU for at most max_waves waves per SIMD (4 SIMDs per CU)
     const int cap_cu = fp.max_waves > 0 ? std::max(1, fp.max_waves * 4 * 64 / block) : INT_MAX;
     const int64_t resident = (int64_t)std::max(1, cus) * std::max(1, std::min(per_cu, cap_cu));
+    // team walk (render_resume_kernel TS > 1): BVH2 item steps only; 0 = auto (launch_walk_team)
+    constexpr bool kTeamable = RESUME && STEP && !WIDE && !LOG;
+    int wteam = 1;
+    if (kTeamable) {
+        wteam = fp.walk_team;
+        if (wteam == 0) wteam = auto_walk_team(fp.nloc, resident * block);
+        if (wteam != 2 && wteam != 4) wteam = 1;
+    }
     // brute-force teams: a tile with fewer pixels than the device has lanes (a row slice of a
     // multi-GPU frame) gives each pixel 4 lanes that split its box tests when it fills at most a quarter of them
     FrameParams f = fp;
@@ -1800,8 +1950,17 @@ hipError_t launch_t(const DevScene& sc, const FrameParams& fp, int block, float*
             f.team = fp.nloc * 4 <= lanes ? 4 : 1;
         }
     }
-    const int64_t need = (fp.nloc * f.team + block - 1) / block;
+    f.walk_team = wteam;
+    const int64_t need = (fp.nloc * f.team * wteam + block - 1) / block;
     int64_t grid = std::min(need, resident);
+    if (kTeamable && wteam > 1) {   // the team instantiation's own occupancy
+        int per_cu_w = 0;
+        const void* wfn = wteam == 2 ? (const void*)render_resume_kernel<COUNT, LOG, SMEM, OVF, STEP, WIDE, kTeamable ? 2 : 1>
+                                     : (const void*)render_resume_kernel<COUNT, LOG, SMEM, OVF, STEP, WIDE, kTeamable ? 4 : 1>;
+        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu_w, wfn, block, lds);
+        if (e != hipSuccess) return e;
+        grid = std::min(need, (int64_t)std::max(1, cus) * std::max(1, std::min(per_cu_w, cap_cu)));
+    }
     // teams run their own instantiation (the ts = 1 kernel keeps the scalar box loop)
     const void* tfn = (const void*)render_kernel<TRAV, COUNT, LOG, SMEM, OVF, BRUTE ? 2 : 0>;
     if (BRUTE && f.team > 1) {
@@ -1817,7 +1976,15 @@ hipError_t launch_t(const DevScene& sc, const FrameParams& fp, int block, float*
                   "work block layout");
     LaunchConst* lc = reinterpret_cast<LaunchConst*>(reinterpret_cast<char*>(d_work) + kConstOffset);
     hipLaunchKernelGGL(make_const_kernel, dim3(1), dim3(64), 0, stream, f, lc);
-    if (RESUME)
+    if (kTeamable && wteam == 2)
+        hipLaunchKernelGGL((render_resume_kernel<COUNT, LOG, SMEM, OVF, STEP, WIDE, kTeamable ? 2 : 1>),
+                           dim3((unsigned)grid), dim3(block), lds, stream, sc, f, d_out, d_counts, d_work,
+                           (const LaunchConst*)lc);
+    else if (kTeamable && wteam == 4)
+        hipLaunchKernelGGL((render_resume_kernel<COUNT, LOG, SMEM, OVF, STEP, WIDE, kTeamable ? 4 : 1>),
+                           dim3((unsigned)grid), dim3(block), lds, stream, sc, f, d_out, d_counts, d_work,
+                           (const LaunchConst*)lc);
+    else if (RESUME)
         hipLaunchKernelGGL((render_resume_kernel<COUNT, LOG, SMEM, OVF, STEP, WIDE>), dim3((unsigned)grid), dim3(block), lds, stream,
                            sc, f, d_out, d_counts, d_work, (const LaunchConst*)lc);
     else if (BRUTE && f.team > 1)

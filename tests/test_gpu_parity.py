@@ -337,6 +337,63 @@ def test_traversal_step_modes_render_identically(kl, case):
         kl.native.set_option("step", 3)
 
 
+@pytest.mark.parametrize("case", ["monkey_c3_64_s4", "serre_96x54_s4", "proto_64_s4", "furnace_64_s4", "grid"])
+def test_team_walk_renders_identically(kl, case):
+    """walk_team: 2 or 4 lanes walk each ray together, stealing the bottom entries of each other's
+    stacks and sharing the best hit -- the hit is the minimum (k, rank) over accepted triangles in any
+    order, so the frame is the one-lane walk's and the oracle's, bit for bit.  Also on row tiles and
+    with the any-hit shadow rays of a scene without glass (grid)."""
+    if case == "grid":
+        sc, cam, env, npix, spp, mb, ibl = W.CONFIGS["C5"].with_size(48, 27, 2).inputs()
+    else:
+        sc, cam, env, npix, spp, mb, ibl = W.PARITY_CASES[case].inputs()
+    kl.native.set_option("brute_max", 0)   # the tree walk, also for small scenes
+    kl.native.set_option("bvh_width", 2)   # teams walk the BVH2 item layout
+    frames, counts = [], []
+    try:
+        for ts in (1, 2, 4):
+            kl.native.set_option("walk_team", ts)
+            frames.append(_launch(kl, sc, cam, env, npix, spp, mb, ibl, "fast"))
+            counts.append(kl.native.count_work_detail(cam, env, npix, spp, mb))
+    finally:
+        kl.native.set_option("walk_team", 0)
+        kl.native.set_option("bvh_width", 0)
+        kl.native.set_option("brute_max", 64)
+    for f in frames[1:]:
+        np.testing.assert_array_equal(frames[0], f)
+    np.testing.assert_array_equal(frames[0], _oracle(sc, cam, env, npix, spp, mb, ibl))
+    # same rays and shading events counted once per team; a team tests at least the nodes one lane does
+    for c in counts[1:]:
+        for k in ("rays", "samples", "ev_diffuse", "ev_glossy", "ev_glass", "sun_terms"):
+            assert c[k] == counts[0][k], k
+    with pytest.raises(_native.NativeError, match="walk_team"):
+        kl.native.set_option("walk_team", 3)
+
+
+@pytest.mark.parametrize("config,spp", [("C3", 16), ("C4", 8)])
+def test_team_walk_row_tiles_full_width(kl, config, spp):
+    """The regime teams are for: a 1/8 row tile of a full-size frame (about one pixel per lane),
+    teams of 2 and 4 vs one lane per pixel, bit for bit."""
+    import torch
+    sc, cam, env, npix, spp_, mb, ibl = W.CONFIGS[config].inputs()
+    _launch(kl, sc, cam, env, npix, 1, mb, ibl, "fast")   # uploads the scene and IBL
+    ctx = kl.native
+    width = int(cam[6])
+    rows = (npix // width + 7) // 8
+    out = torch.empty(3 * width * rows, dtype=torch.float32, device="cuda")
+    frames = []
+    try:
+        for ts in (1, 2, 4):
+            ctx.set_option("walk_team", ts)
+            ctx.render_device(cam, env, npix, spp, mb, 3, 8, out.data_ptr())
+            torch.cuda.synchronize()
+            frames.append(out.cpu().numpy().copy())
+    finally:
+        ctx.set_option("walk_team", 0)
+    for f in frames[1:]:
+        np.testing.assert_array_equal(frames[0], f)
+
+
 @pytest.mark.parametrize("case", ["cornell_64_s4", "monkey_c3_64_s4"])
 def test_resident_wave_cap_renders_identically(kl, case):
     """waves (cap on resident waves per SIMD of the persistent grid) changes which wave renders which

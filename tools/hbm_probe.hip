@@ -1,8 +1,8 @@
 // Calibration probe of the L2 memory-side read counters on gfx950 (VERDICT r02 "prove or drop the
 // 2x FETCH_SIZE correction for 64-B gathers").  Each kernel reads a KNOWN number of bytes with one
 // access pattern; rocprofv3 --pmc passes over this binary give what FETCH_SIZE, TCC_EA0_RDREQ*,
-// TCC_BUBBLE and TCC_EA0_RDREQ_DRAM_32B report for it (tools/hbm_probe.py runs the passes and writes
-// profiles/r03_hbm_probe.json).
+// TCC_BUBBLE and TCC_EA0_RDREQ_DRAM_32B report for it (tools/hbm_probe.sh runs the passes,
+// tools/hbm_probe_summary.py writes profiles/r03_hbm_probe.json).
 //
 //   stream16      16 B per lane, coalesced, over a 1 GiB buffer (the guide's calibrated case)
 //   gather64_mall one random 64-byte record per lane (four 16-byte loads) from a 150 MB table:
@@ -52,8 +52,9 @@ __global__ void __launch_bounds__(256) stream16(const float4* __restrict__ p, ui
     sink(acc, out);
 }
 
-// K records of R bytes (R = 64 or 128) gathered at random, or one 16-byte piece of a 64-byte record
-template <int F4, bool PIECE>
+// K records of R bytes (R = 64 or 128) gathered at random, or one 16-byte piece of a 64-byte record;
+// TAG only gives each probe its own kernel name (0: the 150 MB table, 1: the 4 GiB table)
+template <int F4, bool PIECE, int TAG>
 __global__ void __launch_bounds__(256) gather(const float4* __restrict__ tab, uint32_t nrec, uint32_t seed, float* out) {
     const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
     const uint32_t h = mix(t ^ seed);
@@ -84,10 +85,10 @@ int main() {
     const dim3 blk(256), grd(lanes / 256);
     for (int rep = 0; rep < 2; ++rep) {
         hipLaunchKernelGGL(stream16, dim3(8192), blk, 0, 0, (const float4*)buf, stream / 16, out);
-        hipLaunchKernelGGL((gather<4, false>), grd, blk, 0, 0, (const float4*)buf, (uint32_t)(mall / 64), 11u + rep, out);
-        hipLaunchKernelGGL((gather<4, false>), grd, blk, 0, 0, (const float4*)buf, (uint32_t)(big / 64), 23u + rep, out);
-        hipLaunchKernelGGL((gather<4, true>), grd, blk, 0, 0, (const float4*)buf, (uint32_t)(big / 64), 37u + rep, out);
-        hipLaunchKernelGGL((gather<8, false>), grd, blk, 0, 0, (const float4*)buf, (uint32_t)(big / 128), 41u + rep, out);
+        hipLaunchKernelGGL((gather<4, false, 0>), grd, blk, 0, 0, (const float4*)buf, (uint32_t)(mall / 64), 11u + rep, out);
+        hipLaunchKernelGGL((gather<4, false, 1>), grd, blk, 0, 0, (const float4*)buf, (uint32_t)(big / 64), 23u + rep, out);
+        hipLaunchKernelGGL((gather<4, true, 1>), grd, blk, 0, 0, (const float4*)buf, (uint32_t)(big / 64), 37u + rep, out);
+        hipLaunchKernelGGL((gather<8, false, 1>), grd, blk, 0, 0, (const float4*)buf, (uint32_t)(big / 128), 41u + rep, out);
         CHECK(hipGetLastError());
         CHECK(hipDeviceSynchronize());
     }

@@ -13,16 +13,13 @@ and the ratio of each to the known bytes, so that the correction applied to the 
 counters (tools/summarize_profiles.py) rests on a measured calibration of the same access shape.
 """
 import csv
+import re
 import glob
 import json
 import os
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-KERNELS = {"stream16": "stream16", "gather64_mall": None, "gather64_dram": None, "gather16_dram": None,
-           "gather128_dram": None}
-
-
 def _rows(pattern):
     out = []
     for p in glob.glob(pattern):
@@ -31,16 +28,15 @@ def _rows(pattern):
     return out
 
 
-def kernel_key(name: str, order: dict) -> str:
-    """Map a dispatch to a probe kernel: stream16 by name; the gather<> instantiations by their
-    template arguments and, for the two gather<4, false> tables, by dispatch order."""
+def kernel_key(name: str) -> str:
+    """Map a dispatch to its probe (kernel names: stream16, gather<F4, PIECE, TAG>)."""
     if "stream16" in name:
         return "stream16"
     if "gather<8" in name:
         return "gather128_dram"
-    if "true>" in name:
+    if "true" in name:
         return "gather16_dram"
-    return "gather64"
+    return "gather64_mall" if re.search(r"false, 0>", name) else "gather64_dram"
 
 
 def main(prof, out=None):
@@ -65,18 +61,9 @@ def main(prof, out=None):
                 res.setdefault("kt", []).append((did, name, "ns", float(r["End_Timestamp"]) - float(r["Start_Timestamp"])))
     table = {}
     for sub, rows in res.items():
-        # dispatch order per pass: gather<4,false> dispatches alternate mall, dram within a repetition
-        ids = sorted({(d, n) for d, n, _, _ in rows})
-        g4 = [d for d, n in ids if kernel_key(n, {}) == "gather64"]
-        role = {}
-        for k, d in enumerate(g4):
-            role[d] = "gather64_mall" if k % 2 == 0 else "gather64_dram"
         seen = {}
         for d, n, c, v in sorted(rows):
-            key = kernel_key(n, {})
-            if key == "gather64":
-                key = role[d]
-            seen.setdefault((key, c), []).append(v)
+            seen.setdefault((kernel_key(n), c), []).append(v)
         for (key, c), vs in seen.items():
             table.setdefault(key, {})[c] = vs[-1]   # the second dispatch
     summary = {"source": "tools/hbm_probe.hip under tools/hbm_probe.sh (rocprofv3, one counter group per pass)",
