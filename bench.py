@@ -135,7 +135,8 @@ def roofline(ctx, cnt: dict, kernel_ms: float, pixels: int, workload: str, share
     out["traffic"], out["traffic_frac"] = hbm["traffic"], hbm["traffic_frac"]
     out["hbm_measured"] = {"achieved": (round(traffic / sec / 1e9, 2) if traffic else None), "peak": HBM_PEAK_GBS,
                            "unit": "GB/s", "frac": hbm["traffic_frac"],
-                           "what": "PMC HBM bytes (2 x FETCH_SIZE + WRITE_SIZE, gfx950 correction) / kernel time"}
+                           "what": "PMC memory-side bytes of the same kernel (reads: 128-byte L2 line fills, "
+                                   "calibrated by profiles/r03_hbm_probe.json; + WRITE_SIZE) / kernel time"}
     out["kernel_ms"] = round(kernel_ms, 4)
     out["path"] = (f"brute force ({info['brute_boxes']} distinct leaf boxes, {info['brute_records']} triangles)"
                    if brute else f"SAH tree walk ({info['nodes']} nodes, {info['tris']} triangles)")
@@ -257,6 +258,8 @@ def main():
                     help="FAST tree walk layout: 2 = BVH2, 4 = 4-wide quantised (0 = library default)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extra", action="store_true", help="skip the C3/C4 lines and the host-boundary timing")
+    ap.add_argument("--no-counts", action="store_true",
+                    help="skip the instrumented work-count launch (and the roofline it feeds): profiling passes")
     ap.add_argument("--check", action="store_true",
                     help="N>1: rank 0 re-renders the whole frame alone and compares it with the gathered one")
     args = ap.parse_args()
@@ -363,9 +366,11 @@ def main():
         elapsed, kernel_ms = float(tt[0]), float(tt[1])
 
     # work counters of the same traversal on this rank's tile (instrumented launch, not timed)
-    cnt = ctx.count_work_detail(cam, env, npix, spp, mb, rank, world)
     tile_pixels = D.tile_rows(npix, width, rank, world) * width
-    rf = roofline(ctx, cnt, kernel_ms, tile_pixels, wl.name, share=tile_pixels / npix)
+    rf = None
+    if not args.no_counts:
+        cnt = ctx.count_work_detail(cam, env, npix, spp, mb, rank, world)
+        rf = roofline(ctx, cnt, kernel_ms, tile_pixels, wl.name, share=tile_pixels / npix)
 
     frame_check = None
     if args.check and world > 1:

@@ -72,7 +72,7 @@ def build(verbose: bool = False, force: bool = False, defines=(), out: str = Non
     with ThreadPoolExecutor(max_workers=min(4, max(1, len(jobs)))) as ex:
         list(ex.map(run, jobs))
     if force or jobs or _newer(lib_path, objs):
-        run([hipcc, "--offload-arch=gfx950", "-shared", "-fPIC", "-o", lib_path] + objs)
+        run([hipcc, "--offload-arch=gfx950", "-shared", "-fPIC", "-pthread", "-o", lib_path] + objs)
     return lib_path
 
 

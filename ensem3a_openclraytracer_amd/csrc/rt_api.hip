@@ -18,6 +18,7 @@
 #include <cstring>
 #include <map>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/rt_api.h"
@@ -683,6 +684,7 @@ int check_frame(rt_ctx* ctx, const float* cam, const float* env, int64_t npix, i
     fp->pilot_chunk = 1;
     fp->pilot_levels = 256;
     fp->pilot_state = nullptr;
+    fp->walk_team_dev = nullptr;
     fp->pilot_cost = nullptr;
     fp->pilot_order = nullptr;
     fp->team = ctx->team;
@@ -808,8 +810,8 @@ int rt_set_option(rt_ctx* ctx, const char* key, int64_t value) {
         return RT_OK;
     }
     if (!std::strcmp(key, "walk_team")) {
-        if (value != 0 && value != 1 && value != 2 && value != 4)
-            return set_err(ctx, RT_ERR_ARG, "walk_team must be 0 (auto), 1, 2 or 4");
+        if (value != 0 && value != 1 && value != 2 && value != 4 && value != 8)
+            return set_err(ctx, RT_ERR_ARG, "walk_team must be 0 (auto), 1, 2, 4 or 8");
         ctx->walk_team = (int)value;
         return RT_OK;
     }
@@ -1070,6 +1072,25 @@ int rt_render_device(rt_ctx* ctx, int device_index, const float cam[10], const f
 }
 
 namespace {
+// The host half of the read-back: the pinned stage into the caller's (pageable) array, split over up
+// to 8 threads for frames of several MB (C2's 12.6 MB: one thread ~0.6 ms, the memory bus takes more
+// from several).
+void par_copy(char* dst, const char* src, size_t n) {
+    constexpr size_t kPiece = 2u << 20;
+    const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
+    const size_t k = std::min<size_t>(std::min(8u, hw), n / kPiece);
+    if (k <= 1) {
+        std::memcpy(dst, src, n);
+        return;
+    }
+    const size_t chunk = ((n + k - 1) / k + 4095) & ~(size_t)4095;
+    std::vector<std::thread> ts;
+    for (size_t i = 1; i < k && i * chunk < n; ++i)
+        ts.emplace_back([=] { std::memcpy(dst + i * chunk, src + i * chunk, std::min(chunk, n - i * chunk)); });
+    std::memcpy(dst, src, std::min(chunk, n));
+    for (auto& t : ts) t.join();
+}
+
 // rt_render / rt_render_rgb8: every device renders its rows (row r on device r mod n), then, for
 // rgb8 >= 0, quantizes them on the device (rgb8 = 1: gamma first) so 1 byte per channel crosses
 // PCIe; the host de-interleaves the rows into out (elem = 4 or 1 bytes per channel).
@@ -1123,7 +1144,7 @@ int render_host(rt_ctx* ctx, const float cam[10], const float env[5], int64_t np
         HIP_OR_RET(ctx, hipStreamSynchronize(d.stream));
         const int64_t rows = rt_tile_rows(npix, W, k, nd);
         if (nd == 1) {
-            std::memcpy(dst, d.host_stage, (size_t)npix * 3 * elem);
+            par_copy(dst, d.host_stage, (size_t)npix * 3 * elem);
             continue;
         }
         for (int64_t r = 0; r < rows; ++r) {

@@ -29,6 +29,7 @@ constexpr size_t kWideMinBytes = 16u << 20;
 // kCounterStride bytes apart, then the per-launch constants at kConstOffset.
 constexpr int kGroups = 8;
 constexpr int kCounterStride = 64;
+constexpr int kTeamOffset = 512;    // pilot launches: pixels left after pass 1 (uint32), then the pass-2 team size (int32)
 constexpr int kConstOffset = 1024;
 constexpr int kWorkBytes = 2048;
 // Tile pixels are dealt to the groups in chunks of kChunk consecutive pixels (chunk c to group
@@ -98,7 +99,8 @@ struct FrameParams {
     int64_t nloc;        // pixels in this tile = rows * width
     int32_t resume_min;  // FAST tree walk: resumable traversal, shade once this many lanes are free (0 = off)
     int32_t team;        // brute-force path: lanes per pixel (1, 2, 4, 8; 0 = chosen at launch from the tile size)
-    int32_t walk_team;   // FAST tree walk (BVH2 item steps): lanes per pixel walking each ray together (1, 2, 4; 0 = auto)
+    int32_t walk_team;   // FAST tree walk (BVH2 item steps): lanes per pixel walking each ray together (1, 2, 4, 8; 0 = auto)
+    const int32_t* walk_team_dev;   // pass 2 of a pilot launch with walk_team auto: the team size, chosen on the device
     int32_t max_waves;   // persistent grid: at most this many waves per SIMD (0 = as many as stay resident)
     int32_t step;        // FAST tree walk: 1 = one item per traversal step, 2 = descend-until-leaf rounds, 0 = auto
     // FAST: skip the shadow ray when its result cannot change the sample: envData[3] (sun power) == 0,

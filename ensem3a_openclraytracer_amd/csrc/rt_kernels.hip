@@ -1294,38 +1294,42 @@ __device__ __forceinline__ bool fast_step(const DevScene& S, FastRay& R, const c
 // ---- team traversal: TS lanes walk one ray (tiles with about one pixel per lane, option "walk_team") ----
 // When a tile has no more pixels than the device has lanes, a frame lasts as long as its slowest
 // pixel's chain of samples, and a chain advances one dependent node fetch per step.
-// Here TS consecutive lanes (a team, TS = 2 or 4, inside one DPP quad) carry the same pixel with
+// Here TS consecutive lanes (a team, TS = 2, 4 or 8, aligned) carry the same pixel with
 // identical shading arithmetic and split each ray's tree walk: every lane runs trace_fast's
 // closest-first descent on its own LDS stack, and a lane whose stack runs dry steals the BOTTOM
 // entry (the shallowest: the largest untested subtree) of a teammate's stack.  A lane's stack top
 // evolves exactly as in a one-lane walk started at the subtree it took, so it never holds more than
 // DevScene::depth entries; steals only remove entries from the bottom.  The team's best hit (k, rank,
 // triangle) is reduced across the team (DPP within the quad) in every step where a lane improved it,
-// so culling uses the team's best.  The hit is the minimum (k, rank) over accepted triangles, which
+// so culling uses the team's best (DPP: quad xors, then the half-row mirror for 8).  The hit is the minimum (k, rank) over accepted triangles, which
 // no traversal order changes (every ancestor box is a union of leaf boxes): the frame is the one-lane
 // walk's, bit for bit.
 constexpr int NO_ITEM = INT_MIN;
 
+// One DPP move: M = 1 / 2: lane ^ M within the quad; M = 4: row_half_mirror (lane i <-> 7 - i within
+// 8 lanes), which pairs every lane with one of the other quad of its 8-lane team
 template <int M>
-__device__ __forceinline__ int quad_xor(int x) {   // lane ^ M within the quad (M = 1, 2): one DPP move
-    return __builtin_amdgcn_update_dpp(0, x, M == 1 ? 0xB1 : 0x4E, 0xF, 0xF, false);
+__device__ __forceinline__ int quad_xor(int x) {
+    return __builtin_amdgcn_update_dpp(0, x, M == 1 ? 0xB1 : M == 2 ? 0x4E : 0x141, 0xF, 0xF, false);
 }
 
-// the r-th set bit (r < popcount) of a mask of at most 4 bits (team masks, shifted to bit 0)
+// the r-th set bit (r < popcount) of a team mask (shifted to bit 0)
 __device__ __forceinline__ int nth_bit4(unsigned m, unsigned r) {
     for (unsigned k = 0; k < r; ++k) m &= m - 1u;
     return __builtin_ctz(m);
 }
 
 // One step of a team's walk over the BVH2 item layout (fast_step's loads and arithmetic).  R.item is
-// the lane's own item (NO_ITEM: none), R.soff its stack top and boff its stack bottom (bytes).
-// Returns true (for every lane of the team) when the team's ray is finished.
-template <int TS, bool COUNT, bool SOA, bool OVF>
-__device__ __forceinline__ bool team_step(FastRay& R, unsigned& boff, const char* nb, const char* tb,
+// the lane's own item (NO_ITEM: none), R.soff its stack top and boff its stack bottom (bytes).  ts:
+// lanes per team (2, 4, 8; wave-uniform).  Returns true (for every lane of the team) when the team's
+// ray is finished.
+template <bool COUNT, bool SOA, bool OVF>
+__device__ __forceinline__ bool team_step(int ts, FastRay& R, unsigned& boff, const char* nb, const char* tb,
                                           const LaneStack& st, unsigned kstride, Cnt& c) {
     const unsigned lane = threadIdx.x & 63u;
-    const unsigned tbase = lane & ~(unsigned)(TS - 1);
+    const unsigned tbase = lane & ~(unsigned)(ts - 1);
     const unsigned sub = lane - tbase;
+    const unsigned tm = (1u << ts) - 1u;
     // 1. a lane without an item pops its own stack (entries behind the team's best are discarded)
     if (R.item == NO_ITEM) {
         while (R.soff > boff) {
@@ -1339,8 +1343,8 @@ __device__ __forceinline__ bool team_step(FastRay& R, unsigned& boff, const char
         if (R.soff == boff) R.soff = boff = 0u;   // drained: the next subtree starts a fresh stack
     }
     // 2. lanes still without an item steal the bottom entry of teammates with a non-empty stack
-    const unsigned idle = (unsigned)(__ballot(R.item == NO_ITEM) >> tbase) & ((1u << TS) - 1u);
-    const unsigned vict = (unsigned)(__ballot(R.soff > boff) >> tbase) & ((1u << TS) - 1u);
+    const unsigned idle = (unsigned)(__ballot(R.item == NO_ITEM) >> tbase) & tm;
+    const unsigned vict = (unsigned)(__ballot(R.soff > boff) >> tbase) & tm;
     if (idle && vict) {
         const unsigned nth = (unsigned)__popc(idle), nv = (unsigned)__popc(vict);
         const unsigned below = (1u << sub) - 1u;
@@ -1384,21 +1388,20 @@ __device__ __forceinline__ bool team_step(FastRay& R, unsigned& boff, const char
     if (COUNT) count_wave(c.wave_trav);
     // 4. the team's best: lowest (k, rank) over the team, in every lane
     if (__ballot(improved)) {
-#pragma unroll
-        for (int m = 1; m < TS; m <<= 1) {
-            const float ok = __int_as_float(m == 1 ? quad_xor<1>(__float_as_int(R.bk)) : quad_xor<2>(__float_as_int(R.bk)));
-            const int orank = m == 1 ? quad_xor<1>(R.brank) : quad_xor<2>(R.brank);
-            const int obt = m == 1 ? quad_xor<1>(R.bt) : quad_xor<2>(R.bt);
+        auto fold = [&](float ok, int orank, int obt) __attribute__((always_inline)) {
             if (ok < R.bk || (ok == R.bk && orank < R.brank)) {
                 R.bk = ok;
                 R.brank = orank;
                 R.bt = obt;
             }
-        }
+        };
+        fold(__int_as_float(quad_xor<1>(__float_as_int(R.bk))), quad_xor<1>(R.brank), quad_xor<1>(R.bt));
+        if (ts >= 4) fold(__int_as_float(quad_xor<2>(__float_as_int(R.bk))), quad_xor<2>(R.brank), quad_xor<2>(R.bt));
+        if (ts >= 8) fold(__int_as_float(quad_xor<4>(__float_as_int(R.bk))), quad_xor<4>(R.brank), quad_xor<4>(R.bt));
         if (R.any && R.bt >= 0) return true;   // a shadow ray's hit only matters as hit / miss
     }
     // 5. finished when no lane of the team holds an item or a stack entry
-    const unsigned busy = (unsigned)(__ballot(R.item != NO_ITEM || R.soff > boff) >> tbase) & ((1u << TS) - 1u);
+    const unsigned busy = (unsigned)(__ballot(R.item != NO_ITEM || R.soff > boff) >> tbase) & tm;
     return busy == 0u;
 }
 
@@ -1549,9 +1552,14 @@ constexpr size_t kStepMaxBytes = 16u << 20;
 // them.  C5 ms per frame at 4 / 5 / 6 / 7 / 8 waves: 7,214 / 6,432 / 6,045 / 5,890 / 6,040.  The
 // BVH2 walk (C3/C4) is bound by the vector memory pipeline and keeps 4 waves with its whole 20-entry
 // stack in LDS (5 waves with a 14-entry spilling stack: C3 149 -> 157 ms, C4 475 -> 502 ms).
-constexpr int kWideWaves = 7;
-// TS > 1: teams of TS lanes per pixel walk each ray together (team_step; BVH2 item steps only).
-template <bool COUNT, bool LOG, bool SMEM, bool OVF, bool STEP, bool WIDE, int TS = 1>
+#ifndef RT_WIDE_WAVES
+#define RT_WIDE_WAVES 7   // variant builds (tools/variants.py) override it for the spill A/B
+#endif
+constexpr int kWideWaves = RT_WIDE_WAVES;
+// TEAM: teams of ts lanes per pixel may walk each ray together (team_step; BVH2 item steps only):
+// ts = F.walk_team, or read from F.walk_team_dev (pass 2 of a pilot launch: chosen on the device from
+// the pixels pass 1 left unfinished, pilot_team_kernel).
+template <bool COUNT, bool LOG, bool SMEM, bool OVF, bool STEP, bool WIDE, bool TEAM = false>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WIDE ? kWideWaves : 4))) render_resume_kernel(DevScene S, FrameParams F, float* __restrict__ out,
                                                       unsigned long long* __restrict__ counts,
                                                       unsigned int* __restrict__ work_counter,
@@ -1584,10 +1592,12 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WIDE ?
     const int spp = F.spp, maxB = F.max_bounce;
     const unsigned int nloc = (unsigned int)F.nloc;
     const int lane = threadIdx.x & 63;
-    static_assert(TS == 1 || (TS == 2 || TS == 4) && STEP && !WIDE, "team walk: BVH2 item steps, 2 or 4 lanes");
+    static_assert(!TEAM || (STEP && !WIDE), "team walk: BVH2 item steps");
+    const int TS = !TEAM ? 1 : F.walk_team_dev ? __builtin_amdgcn_readfirstlane(*F.walk_team_dev) : F.walk_team;
     const int team_lane0 = lane & ~(TS - 1);
     const bool team_leader = lane == team_lane0;
-    const unsigned long long team_leaders = TS == 1 ? ~0ull : TS == 2 ? 0x5555555555555555ull : 0x1111111111111111ull;
+    const unsigned long long team_leaders = TS == 1 ? ~0ull : TS == 2 ? 0x5555555555555555ull
+                                            : TS == 4 ? 0x1111111111111111ull : 0x0101010101010101ull;
     unsigned boff = 0;   // team walk: bottom of this lane's stack (bytes; entries below were stolen)
 
     int phase = FETCH;
@@ -1654,7 +1664,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WIDE ?
         ++cost;
         tracing = !fast_init<COUNT>(S, T, o, d, c);
         if (WIDE) T.item = S.wroot_ref;
-        if (TS > 1) {   // the team's first lane takes the root; the others steal from it
+        if (TEAM && TS > 1) {   // the team's first lane takes the root; the others steal from it
             if (!team_leader) T.item = NO_ITEM;
             boff = 0;
         }
@@ -1835,7 +1845,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WIDE ?
         const unsigned long long alive = __ballot(phase != DONE);
         const int rthr = F.resume_min * __popcll(alive);
         while (true) {
-            if (tracing && (TS > 1 ? team_step<TS, COUNT, SMEM, OVF>(T, boff, nb, tb, lst, kstride, c)
+            if (tracing && ((TEAM && TS > 1) ? team_step<COUNT, SMEM, OVF>(TS, T, boff, nb, tb, lst, kstride, c)
                             : WIDE ? (STEP ? wide_step<COUNT, OVF>(T, wnb, wlb, lst, c)
                                            : wide_round<COUNT, OVF>(T, wnb, wlb, lst, c))
                             : STEP ? fast_step<COUNT, SMEM, OVF>(S, T, nb, tb, lst, kstride, c)
@@ -1896,12 +1906,29 @@ __global__ void rgb8_kernel(const float* __restrict__ in, uint8_t* __restrict__ 
     }
 }
 
-// FrameParams::walk_team = 0 (auto): lanes per pixel of the tree walk from the tile's pixels per
-// resident lane (provisional: one lane per pixel until measured)
-inline int auto_walk_team(int64_t nloc, int64_t lanes) {
-    (void)nloc;
-    (void)lanes;
-    return 1;
+// FrameParams::walk_team = 0 (auto): lanes per pixel of the tree walk.  Host rule (one-pass tiles,
+// and pass 1 of a pilot launch) from the tile's pixels per resident lane: teams of 4 at <= 1 pixel
+// per lane (measured on row tiles, profiles/r03_tile_scaling.json: C3 1/8 tile 83 -> 63 ms, C4 1/8
+// tile 355 -> 167 ms, C4 1/4 tile 330 -> 206 ms; at 4-8 pixels per lane teams cost 1.3-2.1x).
+inline int auto_walk_team(int64_t nloc, int64_t lanes) { return nloc <= lanes ? 4 : 1; }
+
+// Device rule (pass 2 of a pilot launch): pass 1 finished every pixel whose samples draw nothing
+// (fixed_point: sky pixels), so the pixels left, u per resident lane, are what pass 2 has to spread:
+// teams of 4 at u <= 1/2, of 2 at u <= 1, else one lane per pixel (r03: C4 1/2 tile u = 0.9, teams
+// of 2 323 vs 348 / 372 ms with 1 / 4 lanes; C3 1/2 tile u = 1.9, one lane 87 vs 106 ms).
+__global__ void pilot_team_count_kernel(const uint32_t* __restrict__ cost, int64_t n, unsigned* __restrict__ left) {
+    unsigned k = 0;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        k += cost[i] != 0u;
+    for (int off = 32; off > 0; off >>= 1) k += __shfl_down(k, off, 64);
+    if ((threadIdx.x & 63) == 0 && k) atomicAdd(left, k);
+}
+
+__global__ void pilot_team_pick_kernel(const unsigned* __restrict__ left, int64_t lanes, int* __restrict__ ts) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        const int64_t u2 = 2 * (int64_t)*left;   // 2 u lanes
+        *ts = u2 <= lanes ? 4 : u2 <= 2 * lanes ? 2 : 1;
+    }
 }
 
 template <int TRAV, bool COUNT, bool LOG, bool SMEM = false, bool RESUME = false, bool OVF = false,
@@ -1928,14 +1955,17 @@ hipError_t launch_t(const DevScene& sc, const FrameParams& fp, int block, float*
     // blocks per CU for at most max_waves waves per SIMD (4 SIMDs per CU)
     const int cap_cu = fp.max_waves > 0 ? std::max(1, fp.max_waves * 4 * 64 / block) : INT_MAX;
     const int64_t resident = (int64_t)std::max(1, cus) * std::max(1, std::min(per_cu, cap_cu));
-    // team walk (render_resume_kernel TS > 1): BVH2 item steps only; 0 = auto (launch_walk_team)
+    // team walk (render_resume_kernel TEAM): BVH2 item steps only.  walk_team_dev: the team size is
+    // chosen on the device (pass 2 of a pilot launch); otherwise walk_team, 0 = auto (auto_walk_team)
     constexpr bool kTeamable = RESUME && STEP && !WIDE && !LOG;
     int wteam = 1;
-    if (kTeamable) {
+    const bool dev_team = kTeamable && fp.walk_team_dev != nullptr;
+    if (kTeamable && !dev_team) {
         wteam = fp.walk_team;
         if (wteam == 0) wteam = auto_walk_team(fp.nloc, resident * block);
-        if (wteam != 2 && wteam != 4) wteam = 1;
+        if (wteam != 2 && wteam != 4 && wteam != 8) wteam = 1;
     }
+    if (dev_team) wteam = 4;   // grid sized for the largest team the device rule picks
     // brute-force teams: a tile with fewer pixels than the device has lanes (a row slice of a
     // multi-GPU frame) gives each pixel 4 lanes that split its box tests when it fills at most a quarter of them
     FrameParams f = fp;
@@ -1951,12 +1981,13 @@ hipError_t launch_t(const DevScene& sc, const FrameParams& fp, int block, float*
         }
     }
     f.walk_team = wteam;
+    if (!dev_team) f.walk_team_dev = nullptr;
+    const bool team_kernel = kTeamable && (dev_team || wteam > 1);
     const int64_t need = (fp.nloc * f.team * wteam + block - 1) / block;
     int64_t grid = std::min(need, resident);
-    if (kTeamable && wteam > 1) {   // the team instantiation's own occupancy
+    const void* wfn = (const void*)render_resume_kernel<COUNT, LOG, SMEM, OVF, STEP, WIDE, kTeamable>;
+    if (team_kernel) {   // the team instantiation's own occupancy
         int per_cu_w = 0;
-        const void* wfn = wteam == 2 ? (const void*)render_resume_kernel<COUNT, LOG, SMEM, OVF, STEP, WIDE, kTeamable ? 2 : 1>
-                                     : (const void*)render_resume_kernel<COUNT, LOG, SMEM, OVF, STEP, WIDE, kTeamable ? 4 : 1>;
         e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu_w, wfn, block, lds);
         if (e != hipSuccess) return e;
         grid = std::min(need, (int64_t)std::max(1, cus) * std::max(1, std::min(per_cu_w, cap_cu)));
@@ -1976,14 +2007,9 @@ hipError_t launch_t(const DevScene& sc, const FrameParams& fp, int block, float*
                   "work block layout");
     LaunchConst* lc = reinterpret_cast<LaunchConst*>(reinterpret_cast<char*>(d_work) + kConstOffset);
     hipLaunchKernelGGL(make_const_kernel, dim3(1), dim3(64), 0, stream, f, lc);
-    if (kTeamable && wteam == 2)
-        hipLaunchKernelGGL((render_resume_kernel<COUNT, LOG, SMEM, OVF, STEP, WIDE, kTeamable ? 2 : 1>),
-                           dim3((unsigned)grid), dim3(block), lds, stream, sc, f, d_out, d_counts, d_work,
-                           (const LaunchConst*)lc);
-    else if (kTeamable && wteam == 4)
-        hipLaunchKernelGGL((render_resume_kernel<COUNT, LOG, SMEM, OVF, STEP, WIDE, kTeamable ? 4 : 1>),
-                           dim3((unsigned)grid), dim3(block), lds, stream, sc, f, d_out, d_counts, d_work,
-                           (const LaunchConst*)lc);
+    if (team_kernel)
+        hipLaunchKernelGGL((render_resume_kernel<COUNT, LOG, SMEM, OVF, STEP, WIDE, kTeamable>), dim3((unsigned)grid),
+                           dim3(block), lds, stream, sc, f, d_out, d_counts, d_work, (const LaunchConst*)lc);
     else if (RESUME)
         hipLaunchKernelGGL((render_resume_kernel<COUNT, LOG, SMEM, OVF, STEP, WIDE>), dim3((unsigned)grid), dim3(block), lds, stream,
                            sc, f, d_out, d_counts, d_work, (const LaunchConst*)lc);
@@ -2266,6 +2292,22 @@ hipError_t launch_render(const DevScene& sc, const FrameParams& fp, int traversa
     hipLaunchKernelGGL(pilot_expand_kernel, dim3(gp), dim3(256), 0, stream, corder, nfull, chunk, fp.nloc, order);
     FrameParams b = fp;
     b.pass = 2;
+    if (fp.walk_team == 0 && traversal == TRAV_FAST) {
+        // pass 2's team size from the pixels pass 1 left unfinished (pilot_team_pick_kernel)
+        static_assert(kTeamOffset >= kGroups * kCounterStride && kTeamOffset + 8 <= kConstOffset, "work block layout");
+        unsigned* left = reinterpret_cast<unsigned*>(reinterpret_cast<char*>(d_work) + kTeamOffset);
+        int* ts = reinterpret_cast<int*>(left + 1);
+        int dev = 0, cus = 0;
+        e = hipGetDevice(&dev);
+        if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+        if (e == hipSuccess) e = hipMemsetAsync(left, 0, sizeof(unsigned), stream);
+        if (e != hipSuccess) return e;
+        hipLaunchKernelGGL(pilot_team_count_kernel, dim3(gp), dim3(256), 0, stream, fp.pilot_cost, fp.nloc, left);
+        // resident lanes of the one-lane BVH2 walk: 4 waves per SIMD
+        hipLaunchKernelGGL(pilot_team_pick_kernel, dim3(1), dim3(64), 0, stream, left,
+                           (int64_t)std::max(cus, 1) * 4 * 4 * 64, ts);
+        b.walk_team_dev = ts;
+    }
     return launch_render_pass(sc, b, traversal, block, d_out, nullptr, d_work, stream);
 }
 

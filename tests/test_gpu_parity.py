@@ -351,7 +351,7 @@ def test_team_walk_renders_identically(kl, case):
     kl.native.set_option("bvh_width", 2)   # teams walk the BVH2 item layout
     frames, counts = [], []
     try:
-        for ts in (1, 2, 4):
+        for ts in (1, 2, 4, 8):
             kl.native.set_option("walk_team", ts)
             frames.append(_launch(kl, sc, cam, env, npix, spp, mb, ibl, "fast"))
             counts.append(kl.native.count_work_detail(cam, env, npix, spp, mb))
@@ -383,7 +383,7 @@ def test_team_walk_row_tiles_full_width(kl, config, spp):
     out = torch.empty(3 * width * rows, dtype=torch.float32, device="cuda")
     frames = []
     try:
-        for ts in (1, 2, 4):
+        for ts in (1, 2, 4, 8):
             ctx.set_option("walk_team", ts)
             ctx.render_device(cam, env, npix, spp, mb, 3, 8, out.data_ptr())
             torch.cuda.synchronize()
@@ -731,6 +731,68 @@ def test_full_size_c5_properties(kl):
     kl.native.render_device(cam, env, npix, spp, mb, 5, 97, t.data_ptr())
     torch.cuda.synchronize()
     np.testing.assert_array_equal(t.cpu().numpy(), f1.reshape(-1, W_ * 3)[5::97].reshape(-1))
+
+
+# FAST (the product default) against the reference's own algorithm at BASELINE sizes.  The REF
+# traversal on the GPU is bit-identical to the CPU oracle wherever the two are compared (every parity
+# case, the whole C2 frame, C3/C4 rows at full spp below), and it is fast enough for whole frames, so
+# whole-frame FAST parity is measured FAST vs REF on the device, with REF pinned to the oracle on a
+# full-spp row of the same frame.  FAST differs only where its reciprocal slab (b-o)*(1/d) and the
+# reference's (b-o)/d round differently at a box face, or where the reference's 20-slot stack drops
+# a subtree (C5's 23-level tree).  Measured non-identical pixels (r03) are pinned:
+# a new divergence fails and has to be explained.
+# The generalisation cases (protoEnsem, FurnaceHD: scenes no auto option was tuned on) run at 1024^2
+# with their own .ini spp and every option on auto.
+FULL_SIZE_WORKLOADS = {
+    "C3": W.CONFIGS["C3"], "C4": W.CONFIGS["C4"], "C5": W.CONFIGS["C5"],
+    "proto": W.Workload("proto_1024_s100", "proto", 1024, 1024, 100),
+    "furnace": W.Workload("furnace_1024_s1000", "furnace", 1024, 1024, 1000),
+}
+FULL_SIZE_FAST = {
+    # config: (spp, rows (row0, row_step) or None = whole frame, oracle row, the measured set of
+    # non-identical pixels (r03, one MI355X): C3 5 of 1,048,576 (max per-pixel L2 0.0039), proto 1)
+    "C3": (256, None, 517, {91029, 156256, 490876, 529159, 856344}),
+    "C4": (32, None, 611, set()),
+    "C5": (1024, (700, 1000), 700, set()),
+    "proto": (100, None, 389, {678387}),
+    "furnace": (1000, None, 611, set()),
+}
+
+
+@pytest.mark.parametrize("config", list(FULL_SIZE_FAST))
+def test_full_size_fast_vs_ref_pixel_counts(kl, config):
+    import json
+    import torch
+    spp_cfg, tile, orow, pinned = FULL_SIZE_FAST[config]
+    sc, cam, env, npix, _, mb, ibl = FULL_SIZE_WORKLOADS[config].inputs()
+    W_ = int(cam[6])
+    row0, step = tile if tile else (0, 1)
+    _launch(kl, sc, cam, env, npix, 1, mb, ibl, "fast")   # uploads the scene and IBL
+    from ensem3a_openclraytracer_amd import distributed as D
+    rows = D.tile_rows(npix, W_, row0, step)
+    out = torch.empty(3 * W_ * rows, dtype=torch.float32, device="cuda")
+    frames = {}
+    try:
+        for trav in ("ref", "fast"):
+            kl.native.set_option("traversal", _native.RT_TRAVERSAL_REF if trav == "ref" else _native.RT_TRAVERSAL_FAST)
+            kl.native.render_device(cam, env, npix, spp_cfg, mb, row0, step, out.data_ptr())
+            torch.cuda.synchronize()
+            frames[trav] = out.cpu().numpy().copy()
+    finally:
+        kl.native.set_option("traversal", _native.RT_TRAVERSAL_FAST)
+    st = compare.assert_gate(frames["fast"], frames["ref"], f"{config} FAST vs REF")
+    diff = np.unique(np.nonzero(frames["fast"] != frames["ref"])[0] // 3)
+    # REF pinned to the oracle on one full-width row of the same frame
+    ridx = (orow - row0) // step
+    assert (orow - row0) % step == 0 and 0 <= ridx < rows
+    ora = _oracle(sc, cam, env, npix, spp_cfg, mb, ibl, row0=orow, row_step=npix // W_ + 1)
+    np.testing.assert_array_equal(frames["ref"].reshape(rows, W_ * 3)[ridx], ora)
+    print(json.dumps({"config": config, "spp": spp_cfg, "pixels": int(rows * W_), "non_identical": int(diff.size),
+                      "frac_identical": st["frac_identical"], "max_l2": st["max_l2"], "rmse": st["rmse"],
+                      "first": [int(x) for x in diff[:8]]}))
+    assert set(diff.tolist()) <= pinned, (diff.size, diff[:20])
+    f = frames["fast"]
+    assert np.isfinite(f).all() and 0.0 <= f.min() and f.max() <= 1.0
 
 
 @pytest.mark.parametrize("case", ["monkey_c3_64_s4", "serre_96x54_s4", "proto_64_s4", "furnace_64_s4", "grid"])

@@ -4,9 +4,16 @@
 
 Writes profiles/TAG_kernel_stats_WORKLOAD.csv (the --stats table of the kernel-trace run) and
 profiles/TAG_pmc_WORKLOAD.json: per-launch means of every counter of the render kernel, and
-  hbm_bytes_per_launch = (2 x FETCH_SIZE + WRITE_SIZE) KiB -> bytes, corrected as
-      MI355X_MICROARCH.md prescribes for gfx950 (FETCH_SIZE counts half of a wide read's bytes;
-      WRITE_SIZE exact);
+  hbm_read_bytes_per_launch = 128 x TCC_EA0_RDREQ_128B + 64 x RDREQ_64B + 32 x RDREQ_32B: the bytes the
+      L2 moved from memory (HBM or the Infinity Cache), every request at its size.  Calibrated by
+      tools/hbm_probe.hip (profiles/r03_hbm_probe.json): on gfx950 the L2 fetches a whole 128-byte line
+      per miss, for 16-byte streaming reads and for 16/64/128-byte random gathers alike, and the
+      by-size sum equals the known bytes of a 128-byte gather and of a streaming read (0.999-1.000);
+      FETCH_SIZE tallies each 128-byte request at 64 B (TCC_BUBBLE reads 0), i.e. exactly half.  A
+      64-byte record gathered at random therefore costs 128 bytes of memory traffic, two records'
+      worth (hbm_line_bytes_per_request = 128).  Without the request-size pass: 2 x FETCH_SIZE.
+  hbm_bytes_per_launch = hbm_read_bytes_per_launch + WRITE_SIZE (writes: exact for streaming
+      stores, MI355X_MICROARCH.md);
   valu_lane_slots_per_launch = SQ_INSTS_VALU x 64 (wave-level VALU instructions x lanes);
   valu_lane_util = SQ_THREAD_CYCLES_VALU / (64 x SQ_ACTIVE_INST_VALU) (active lanes per VALU issue);
   valu_issue_frac = valu_lane_slots_per_launch / kernel time / 78.64e12 lane-ops/s.
@@ -49,7 +56,7 @@ def main(prof, tag, workload, frames=None, kernel=KERNEL):
                 s["frames"] = int(frames) if frames else int(r["Calls"])
                 s["kernel_avg_ms"] = float(r["TotalDurationNs"]) / 1e6 / s["frames"]
     counters = {}
-    for sub in ("fetch", "write", "dram", "sq"):
+    for sub in ("fetch", "write", "dram", "req", "sq"):
         for r in _rows(os.path.join(prof, sub, "*counter_collection.csv")):
             if re.search(kernel, r["Kernel_Name"]):
                 counters.setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))
@@ -58,9 +65,16 @@ def main(prof, tag, workload, frames=None, kernel=KERNEL):
         s[k + "_per_launch"] = float(np.mean(v)) * per
         s[k + "_launches"] = len(v)
     g = lambda k: s.get(k + "_per_launch")  # noqa: E731
-    if g("FETCH_SIZE") is not None and g("WRITE_SIZE") is not None:
-        s["hbm_bytes_per_launch"] = (2.0 * g("FETCH_SIZE") + g("WRITE_SIZE")) * 1024
-        s["hbm_bytes_note"] = "(2 x FETCH_SIZE + WRITE_SIZE) KiB: gfx950 half-count correction of FETCH_SIZE"
+    if g("TCC_EA0_RDREQ_128B_sum") is not None:
+        s["hbm_read_bytes_per_launch"] = (128.0 * g("TCC_EA0_RDREQ_128B_sum") + 64.0 * (g("TCC_EA0_RDREQ_64B_sum") or 0.0)
+                                          + 32.0 * (g("TCC_EA0_RDREQ_32B_sum") or 0.0))
+        s["hbm_read_note"] = "128 x RDREQ_128B + 64 x RDREQ_64B + 32 x RDREQ_32B (profiles/r03_hbm_probe.json)"
+    elif g("FETCH_SIZE") is not None:
+        s["hbm_read_bytes_per_launch"] = 2.0 * g("FETCH_SIZE") * 1024
+        s["hbm_read_note"] = "2 x FETCH_SIZE KiB (every request a 128-byte line, profiles/r03_hbm_probe.json)"
+    if s.get("hbm_read_bytes_per_launch") is not None and g("WRITE_SIZE") is not None:
+        s["hbm_bytes_per_launch"] = s["hbm_read_bytes_per_launch"] + g("WRITE_SIZE") * 1024
+        s["hbm_bytes_note"] = "memory-side reads (128-byte lines, calibrated) + WRITE_SIZE"
         if s.get("kernel_avg_ms"):
             s["hbm_GBps"] = s["hbm_bytes_per_launch"] / (s["kernel_avg_ms"] * 1e-3) / 1e9
             s["hbm_frac_of_8TBps"] = s["hbm_GBps"] / 8000.0
