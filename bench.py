@@ -79,9 +79,11 @@ def _dist_env():
     return rank, world, local
 
 
-def _profile(config_name: str):
-    """The newest committed rocprofv3 PMC summary for this workload (profiles/*pmc*<workload>*.json)."""
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"*pmc*{config_name}*.json")))
+def _profile(config_name: str, ab: str = ""):
+    """The newest committed rocprofv3 PMC summary for this workload (profiles/rNN_pmc_<workload>.json;
+    ab: an A/B variant's summary, profiles/rNN_ab_<ab>_pmc_<workload>.json)."""
+    pat = f"r*_ab_{ab}_pmc_{config_name}.json" if ab else f"r*_pmc_{config_name}.json"
+    files = sorted(f for f in glob.glob(os.path.join(ROOT, "profiles", pat)) if ab or "_ab_" not in f)
     if not files:
         return {}
     try:
@@ -137,6 +139,18 @@ def roofline(ctx, cnt: dict, kernel_ms: float, pixels: int, workload: str, share
                            "unit": "GB/s", "frac": hbm["traffic_frac"],
                            "what": "PMC memory-side bytes of the same kernel (reads: 128-byte L2 line fills, "
                                    "calibrated by profiles/r03_hbm_probe.json; + WRITE_SIZE) / kernel time"}
+    # the spill-free A/B build of the same walk (4 waves per SIMD, no scratch, 20 LDS stack entries):
+    # its memory-side bytes are the walk's own line fills + the frame, i.e. the useful part of the
+    # default build's traffic; the rest of the default build's bytes are register spills and stack
+    # entries beyond the LDS part
+    ab = _profile(workload, "w4")
+    if traffic and ab.get("hbm_bytes_per_launch"):
+        useful = ab["hbm_bytes_per_launch"] * share
+        out["hbm_measured"]["useful"] = {
+            "bytes_per_launch": useful, "achieved": round(useful / sec / 1e9, 2), "peak": HBM_PEAK_GBS,
+            "frac": round(useful / sec / 1e9 / HBM_PEAK_GBS, 5), "spill_bytes_per_launch": traffic - useful,
+            "what": "BVH / triangle line fills + frame writes: the memory-side bytes of the spill-free 4-wave "
+                    "build of the same walk (" + ab.get("_file", "") + "), over this build's kernel time"}
     out["kernel_ms"] = round(kernel_ms, 4)
     out["path"] = (f"brute force ({info['brute_boxes']} distinct leaf boxes, {info['brute_records']} triangles)"
                    if brute else f"SAH tree walk ({info['nodes']} nodes, {info['tris']} triangles)")

@@ -1556,14 +1556,17 @@ constexpr size_t kStepMaxBytes = 16u << 20;
 #define RT_WIDE_WAVES 7   // variant builds (tools/variants.py) override it for the spill A/B
 #endif
 constexpr int kWideWaves = RT_WIDE_WAVES;
-// TEAM: teams of ts lanes per pixel may walk each ray together (team_step; BVH2 item steps only):
-// ts = F.walk_team, or read from F.walk_team_dev (pass 2 of a pilot launch: chosen on the device from
-// the pixels pass 1 left unfinished, pilot_team_kernel).
-template <bool COUNT, bool LOG, bool SMEM, bool OVF, bool STEP, bool WIDE, bool TEAM = false>
+// TS > 1: teams of TS lanes per pixel walk each ray together (team_step; BVH2 item steps only).
+// F.walk_team_dev (pass 2 of a pilot launch): the team size was chosen on the device from the pixels
+// pass 1 left unfinished (pilot_team_pick_kernel); the instantiations of the other sizes, launched
+// beside this one, return at once.
+template <bool COUNT, bool LOG, bool SMEM, bool OVF, bool STEP, bool WIDE, int TS = 1>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WIDE ? kWideWaves : 4))) render_resume_kernel(DevScene S, FrameParams F, float* __restrict__ out,
                                                       unsigned long long* __restrict__ counts,
                                                       unsigned int* __restrict__ work_counter,
                                                       const LaunchConst* __restrict__ lconst) {
+    // pass 2 with the team size chosen on the device: only the instantiation of that size renders
+    if (F.walk_team_dev && __builtin_amdgcn_readfirstlane(*F.walk_team_dev) != TS) return;
     extern __shared__ int lds_stack[];
     const int B = blockDim.x;
     Cnt c{};
@@ -1592,8 +1595,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WIDE ?
     const int spp = F.spp, maxB = F.max_bounce;
     const unsigned int nloc = (unsigned int)F.nloc;
     const int lane = threadIdx.x & 63;
-    static_assert(!TEAM || (STEP && !WIDE), "team walk: BVH2 item steps");
-    const int TS = !TEAM ? 1 : F.walk_team_dev ? __builtin_amdgcn_readfirstlane(*F.walk_team_dev) : F.walk_team;
+    static_assert(TS == 1 || ((TS == 2 || TS == 4 || TS == 8) && STEP && !WIDE), "team walk: BVH2 item steps");
     const int team_lane0 = lane & ~(TS - 1);
     const bool team_leader = lane == team_lane0;
     const unsigned long long team_leaders = TS == 1 ? ~0ull : TS == 2 ? 0x5555555555555555ull
@@ -1664,7 +1666,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WIDE ?
         ++cost;
         tracing = !fast_init<COUNT>(S, T, o, d, c);
         if (WIDE) T.item = S.wroot_ref;
-        if (TEAM && TS > 1) {   // the team's first lane takes the root; the others steal from it
+        if (TS > 1) {   // the team's first lane takes the root; the others steal from it
             if (!team_leader) T.item = NO_ITEM;
             boff = 0;
         }
@@ -1845,7 +1847,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WIDE ?
         const unsigned long long alive = __ballot(phase != DONE);
         const int rthr = F.resume_min * __popcll(alive);
         while (true) {
-            if (tracing && ((TEAM && TS > 1) ? team_step<COUNT, SMEM, OVF>(TS, T, boff, nb, tb, lst, kstride, c)
+            if (tracing && (TS > 1 ? team_step<COUNT, SMEM, OVF>(TS, T, boff, nb, tb, lst, kstride, c)
                             : WIDE ? (STEP ? wide_step<COUNT, OVF>(T, wnb, wlb, lst, c)
                                            : wide_round<COUNT, OVF>(T, wnb, wlb, lst, c))
                             : STEP ? fast_step<COUNT, SMEM, OVF>(S, T, nb, tb, lst, kstride, c)
@@ -1965,7 +1967,7 @@ hipError_t launch_t(const DevScene& sc, const FrameParams& fp, int block, float*
         if (wteam == 0) wteam = auto_walk_team(fp.nloc, resident * block);
         if (wteam != 2 && wteam != 4 && wteam != 8) wteam = 1;
     }
-    if (dev_team) wteam = 4;   // grid sized for the largest team the device rule picks
+
     // brute-force teams: a tile with fewer pixels than the device has lanes (a row slice of a
     // multi-GPU frame) gives each pixel 4 lanes that split its box tests when it fills at most a quarter of them
     FrameParams f = fp;
@@ -1982,15 +1984,25 @@ hipError_t launch_t(const DevScene& sc, const FrameParams& fp, int block, float*
     }
     f.walk_team = wteam;
     if (!dev_team) f.walk_team_dev = nullptr;
-    const bool team_kernel = kTeamable && (dev_team || wteam > 1);
     const int64_t need = (fp.nloc * f.team * wteam + block - 1) / block;
     int64_t grid = std::min(need, resident);
-    const void* wfn = (const void*)render_resume_kernel<COUNT, LOG, SMEM, OVF, STEP, WIDE, kTeamable>;
-    if (team_kernel) {   // the team instantiation's own occupancy
+    // the team instantiations (TS = 2, 4, 8) and their own occupancy
+    auto team_fn = [&](int ts) -> const void* {
+        if (!kTeamable) return nullptr;
+        return ts == 2 ? (const void*)render_resume_kernel<COUNT, LOG, SMEM, OVF, STEP, WIDE, kTeamable ? 2 : 1>
+             : ts == 4 ? (const void*)render_resume_kernel<COUNT, LOG, SMEM, OVF, STEP, WIDE, kTeamable ? 4 : 1>
+                       : (const void*)render_resume_kernel<COUNT, LOG, SMEM, OVF, STEP, WIDE, kTeamable ? 8 : 1>;
+    };
+    auto team_grid = [&](int ts, int64_t* g) -> hipError_t {
         int per_cu_w = 0;
-        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu_w, wfn, block, lds);
+        hipError_t er = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu_w, team_fn(ts), block, lds);
+        *g = std::min((fp.nloc * ts + block - 1) / block,
+                      (int64_t)std::max(1, cus) * std::max(1, std::min(per_cu_w, cap_cu)));
+        return er;
+    };
+    if (kTeamable && wteam > 1 && !dev_team) {
+        e = team_grid(wteam, &grid);
         if (e != hipSuccess) return e;
-        grid = std::min(need, (int64_t)std::max(1, cus) * std::max(1, std::min(per_cu_w, cap_cu)));
     }
     // teams run their own instantiation (the ts = 1 kernel keeps the scalar box loop)
     const void* tfn = (const void*)render_kernel<TRAV, COUNT, LOG, SMEM, OVF, BRUTE ? 2 : 0>;
@@ -2007,9 +2019,33 @@ hipError_t launch_t(const DevScene& sc, const FrameParams& fp, int block, float*
                   "work block layout");
     LaunchConst* lc = reinterpret_cast<LaunchConst*>(reinterpret_cast<char*>(d_work) + kConstOffset);
     hipLaunchKernelGGL(make_const_kernel, dim3(1), dim3(64), 0, stream, f, lc);
-    if (team_kernel)
-        hipLaunchKernelGGL((render_resume_kernel<COUNT, LOG, SMEM, OVF, STEP, WIDE, kTeamable>), dim3((unsigned)grid),
+    if (kTeamable && dev_team) {
+        // the device picks 1, 2 or 4 (pilot_team_pick_kernel): all three are launched in order, and the
+        // two whose size was not picked return at once
+        int64_t g2 = 0, g4 = 0;
+        e = team_grid(2, &g2);
+        if (e == hipSuccess) e = team_grid(4, &g4);
+        if (e != hipSuccess) return e;
+        hipLaunchKernelGGL((render_resume_kernel<COUNT, LOG, SMEM, OVF, STEP, WIDE, 1>), dim3((unsigned)grid),
                            dim3(block), lds, stream, sc, f, d_out, d_counts, d_work, (const LaunchConst*)lc);
+        hipLaunchKernelGGL((render_resume_kernel<COUNT, LOG, SMEM, OVF, STEP, WIDE, kTeamable ? 2 : 1>),
+                           dim3((unsigned)g2), dim3(block), lds, stream, sc, f, d_out, d_counts, d_work,
+                           (const LaunchConst*)lc);
+        hipLaunchKernelGGL((render_resume_kernel<COUNT, LOG, SMEM, OVF, STEP, WIDE, kTeamable ? 4 : 1>),
+                           dim3((unsigned)g4), dim3(block), lds, stream, sc, f, d_out, d_counts, d_work,
+                           (const LaunchConst*)lc);
+    } else if (kTeamable && wteam == 2)
+        hipLaunchKernelGGL((render_resume_kernel<COUNT, LOG, SMEM, OVF, STEP, WIDE, kTeamable ? 2 : 1>),
+                           dim3((unsigned)grid), dim3(block), lds, stream, sc, f, d_out, d_counts, d_work,
+                           (const LaunchConst*)lc);
+    else if (kTeamable && wteam == 4)
+        hipLaunchKernelGGL((render_resume_kernel<COUNT, LOG, SMEM, OVF, STEP, WIDE, kTeamable ? 4 : 1>),
+                           dim3((unsigned)grid), dim3(block), lds, stream, sc, f, d_out, d_counts, d_work,
+                           (const LaunchConst*)lc);
+    else if (kTeamable && wteam == 8)
+        hipLaunchKernelGGL((render_resume_kernel<COUNT, LOG, SMEM, OVF, STEP, WIDE, kTeamable ? 8 : 1>),
+                           dim3((unsigned)grid), dim3(block), lds, stream, sc, f, d_out, d_counts, d_work,
+                           (const LaunchConst*)lc);
     else if (RESUME)
         hipLaunchKernelGGL((render_resume_kernel<COUNT, LOG, SMEM, OVF, STEP, WIDE>), dim3((unsigned)grid), dim3(block), lds, stream,
                            sc, f, d_out, d_counts, d_work, (const LaunchConst*)lc);

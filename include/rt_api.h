@@ -82,8 +82,14 @@ int rt_set_env(rt_ctx* ctx, const uint8_t* rgba, int w, int h);
  * hits), "step" (resumable tree walk: 1 = one node or leaf per traversal
  * step, 2 = descend to a leaf per step, 0 = auto by node-array size -- same
  * hits), "team" (brute force: lanes per pixel 1/2/4/8, 0 = auto by tile
- * size), "waves" (persistent grid: at most this many waves per SIMD, 0 =
- * occupancy limit), "block" (threads per block: 64, 128 or 256).
+ * size), "walk_team" (BVH2 tree walk: 1/2/4/8 lanes walk each ray of a pixel
+ * together, 0 = auto: 4 on tiles of at most one pixel per resident lane and
+ * on the second pass of a pilot launch from the pixels its first pass left --
+ * same hits), "waves" (persistent grid: at most this many waves per SIMD, 0 =
+ * occupancy limit), "block" (threads per block: 64, 128 or 256), and the
+ * tuning switches documented in DESIGN.md 4.2 ("sun_skip", "sun_any",
+ * "fixed_point", "pilot", "pilot_chunk", "pilot_levels", "stack_lds",
+ * "bvh_width"): every option renders the same frame.
  * "bvh" and "brute_max" may be changed after rt_set_scene. */
 int rt_set_option(rt_ctx* ctx, const char* key, int64_t value);
 
