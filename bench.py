@@ -170,10 +170,29 @@ def roofline(ctx, cnt: dict, kernel_ms: float, pixels: int, workload: str, share
     return out
 
 
+def host_cores() -> dict:
+    """The host CPUs this job may run on: the cgroup CPU quota (cpu.max) when there is one, else the
+    affinity mask.  On the GPU box the quota is 16 CPUs of a 256-CPU machine (nproc = 16): more
+    threads than that time-slice the same 16 CPUs."""
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, period = f.read().split()[:2]
+        if q != "max":
+            quota = max(1, int(int(q) // int(period)))
+    except (OSError, ValueError):
+        pass
+    cores = min(aff, quota) if quota else aff
+    return {"cores": cores, "affinity_cpus": aff, "cgroup_cpu_quota": quota, "cpu_count": os.cpu_count()}
+
+
 def cpu_baseline(wl, scene, ibl, cam, env, target_s: float = 10.0):
-    """Time the CPU oracle on a row sample of the frame (rows row0::step at full spp)."""
+    """Time the CPU oracle on a row sample of the frame (rows row0::step at full spp), one OpenMP
+    thread per host CPU the job may use (host_cores)."""
     import oracle.oracle as O
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+    hc = host_cores()
+    threads = hc["cores"]
     osc = O.OracleScene.from_scene(scene, ibl)
     W = int(cam[6])
     H = (wl.npix + W - 1) // W
@@ -188,7 +207,7 @@ def cpu_baseline(wl, scene, ibl, cam, env, target_s: float = 10.0):
         step = max(1, min(step // 2, int(step * dt / target_s)))
     rows = (H + step - 1) // step
     samples = rows * W * wl.spp
-    return {"value": samples / dt / 1e6, "unit": "Msamples/s", "cores": threads, "kind": "port",
+    return {"value": samples / dt / 1e6, "unit": "Msamples/s", "cores": threads, "kind": "port", "host": hc,
             "sample": f"rows 0::{step} of the {W}x{H} frame ({rows} rows) at {wl.spp} spp = {samples} samples "
                       f"in {dt:.2f} s; oracle/rt_oracle.c (C restatement of the reference kernel), OpenMP",
             "calibration": "C2 in the build container, 8 threads: oracle 1.90 Msamples/s vs the reference kernel "

@@ -48,21 +48,29 @@ def main(prof, tag, workload, frames=None, kernel=KERNEL):
     stats = glob.glob(os.path.join(prof, "kt", "*kernel_stats.csv"))
     s = {"workload": workload, "kernel": kernel, "source": "rocprofv3 (tools/run_profiles.sh)"}
     if stats:
+        # every instantiation of the render kernel counts (two-pass launches: pass 1 and pass 2; a
+        # device-chosen team size launches the other sizes' instantiations, which return at once)
         shutil.copy(stats[0], os.path.join(ROOT, "profiles", f"{tag}_kernel_stats_{workload}.csv"))
+        names, calls, total = [], 0, 0.0
         for r in _rows(stats[0]):
             if re.search(kernel, r["Name"]):
-                s["kernel_name"] = r["Name"][:120]
-                s["kernel_calls"] = int(r["Calls"])
-                s["frames"] = int(frames) if frames else int(r["Calls"])
-                s["kernel_avg_ms"] = float(r["TotalDurationNs"]) / 1e6 / s["frames"]
+                names.append(r["Name"][:120])
+                calls += int(r["Calls"])
+                total += float(r["TotalDurationNs"])
+        if names:
+            s["kernel_name"] = names[0] if len(names) == 1 else names
+            s["kernel_calls"] = calls
+            s["frames"] = int(frames) if frames else calls
+            s["kernel_avg_ms"] = total / 1e6 / s["frames"]
     counters = {}
     for sub in ("fetch", "write", "dram", "req", "sq"):
         for r in _rows(os.path.join(prof, sub, "*counter_collection.csv")):
             if re.search(kernel, r["Kernel_Name"]):
                 counters.setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))
-    per = s.get("kernel_calls", 1) / max(1, s.get("frames", 1))   # dispatches per frame
+    nframes = max(1, s.get("frames", 1))
     for k, v in sorted(counters.items()):
-        s[k + "_per_launch"] = float(np.mean(v)) * per
+        # per frame: every dispatch of the frame summed (the profiled run renders `frames` frames)
+        s[k + "_per_launch"] = float(np.sum(v)) / nframes
         s[k + "_launches"] = len(v)
     g = lambda k: s.get(k + "_per_launch")  # noqa: E731
     if g("TCC_EA0_RDREQ_128B_sum") is not None:
