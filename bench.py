@@ -30,8 +30,9 @@ Extra fields (DESIGN.md 5 derives every number):
                    (SQ_INSTS_VALU x 64) per launch, when committed.
   host_boundary -- rt_render (launch_Raytracing's blocking C-ABI: kernel + copy of
                    the frame into caller memory), timed over the same W/K steps.
-  configs       -- N=1 only: C3 and C4 timed the same way (2 steps, 1 warmup), C5 (1 step, 1
-                   warmup: 5-6 s per frame).
+  configs       -- C3 and C4 timed the same way (2 steps, 1 warmup), C5 (1 step, 1 warmup: 5-6 s
+                   per frame); at N=1 on one device (with their roofline), at N>1 through the same
+                   row tiles + RCCL gather as the headline (every config's strong scaling).
   cpu_baseline  -- the CPU oracle (a C restatement of the reference kernel, OpenMP)
                    timed on this host on a bounded row sample of the same frame.
 """
@@ -333,6 +334,68 @@ def main():
             c.set_option(k, int(v))
         return c
 
+    def run_frames(ctx, cam, env, npix, spp, mb, steps, warmup):
+        """Render `steps` frames of one config after `warmup` untimed ones: every rank its row tile
+        (rt_render_device, scene resident), rank 0 gathers the tiles over RCCL and assembles each frame
+        (frame k's gather overlaps frame k+1's render: two tile buffers).  Returns (elapsed s, mean
+        kernel ms, the last assembled frame on rank 0), both times the max over ranks."""
+        width = int(cam[6])
+        stream = torch.cuda.current_stream()
+        mrows = D.max_tile_rows(npix, width, world)
+        nbuf = 2 if world > 1 else 1
+        tiles = [torch.zeros(3 * width * mrows, dtype=torch.float32, device="cuda") for _ in range(nbuf)]
+        bufs = [[torch.empty(tiles[0].numel(), dtype=torch.float32, device=coll) for _ in range(world)]
+                for _ in range(nbuf)] if (world > 1 and rank == 0) else [None] * nbuf
+        frame = torch.empty(3 * npix, dtype=torch.float32, device=coll) if (rank == 0 and world > 1) else None
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+        pending = []   # (work, buffer index) of the gather in flight
+
+        def finish_pending():
+            while pending:
+                work, b = pending.pop(0)
+                if work is not None:
+                    work.wait()   # the current stream waits for the gather (no host block for RCCL)
+                if rank == 0:
+                    D.assemble(bufs[b], width, npix, world, out=frame)
+
+        def step(i=None, k=0):
+            b = k % nbuf
+            if i is not None:
+                ev[i][0].record(stream)
+            ctx.render_device(cam, env, npix, spp, mb, rank, world, tiles[b].data_ptr(), stream.cuda_stream)
+            if i is not None:
+                ev[i][1].record(stream)
+            if world > 1:
+                if coll == "cuda":
+                    work = dist.gather(tiles[b], gather_list=bufs[b], dst=0, async_op=True)
+                else:   # one-GPU gloo rehearsal: host copies, synchronous
+                    dist.gather(tiles[b].cpu(), gather_list=bufs[b], dst=0)
+                    work = None
+                finish_pending()      # the previous frame's gather ran while this frame rendered
+                pending.append((work, b))
+
+        for w in range(warmup):
+            step(k=w)
+        finish_pending()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for i in range(steps):
+            step(i, k=i)
+        finish_pending()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        elapsed = time.perf_counter() - t0
+        kms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+        if world > 1:
+            tt = torch.tensor([elapsed, kms], dtype=torch.float64, device=coll)
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+            elapsed, kms = float(tt[0]), float(tt[1])
+        return elapsed, kms, frame
+
     wl = Wk.CONFIGS[args.config]
     scene, cam, env, npix, spp, mb, ibl = wl.inputs()
     ctx = make_ctx()
@@ -340,63 +403,7 @@ def main():
     ctx.set_env(ibl)
     width = int(cam[6])
     stream = torch.cuda.current_stream()
-    mrows = D.max_tile_rows(npix, width, world)
-    # N > 1: two tile buffers, so that frame k's RCCL gather (on the collective's own stream) overlaps
-    # frame k+1's render; rank 0 assembles frame k once its gather is done
-    nbuf = 2 if world > 1 else 1
-    tiles = [torch.zeros(3 * width * mrows, dtype=torch.float32, device="cuda") for _ in range(nbuf)]
-    tile = tiles[0]
-    bufs = [[torch.empty(tile.numel(), dtype=torch.float32, device=coll) for _ in range(world)] for _ in range(nbuf)] \
-        if (world > 1 and rank == 0) else [None] * nbuf
-    frame = torch.empty(3 * npix, dtype=torch.float32, device=coll) if (rank == 0 and world > 1) else None
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
-    pending = []   # (work, buffer index) of the gather in flight
-
-    def finish_pending():
-        while pending:
-            work, b = pending.pop(0)
-            if work is not None:
-                work.wait()   # the current stream waits for the gather (no host block for RCCL)
-            if rank == 0:
-                D.assemble(bufs[b], width, npix, world, out=frame)
-
-    def step(i=None, k=0):
-        b = k % nbuf
-        if i is not None:
-            ev[i][0].record(stream)
-        ctx.render_device(cam, env, npix, spp, mb, rank, world, tiles[b].data_ptr(), stream.cuda_stream)
-        if i is not None:
-            ev[i][1].record(stream)
-        if world > 1:
-            if coll == "cuda":
-                work = dist.gather(tiles[b], gather_list=bufs[b], dst=0, async_op=True)
-            else:   # one-GPU gloo rehearsal: host copies, synchronous
-                dist.gather(tiles[b].cpu(), gather_list=bufs[b], dst=0)
-                work = None
-            finish_pending()      # the previous frame's gather ran while this frame rendered
-            pending.append((work, b))
-
-    for w in range(args.warmup):
-        step(k=w)
-    finish_pending()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for i in range(args.steps):
-        step(i, k=i)
-    finish_pending()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    t1 = time.perf_counter()
-    elapsed = t1 - t0
-    kernel_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
-    if world > 1:
-        tt = torch.tensor([elapsed, kernel_ms], dtype=torch.float64, device=coll)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        elapsed, kernel_ms = float(tt[0]), float(tt[1])
+    elapsed, kernel_ms, frame = run_frames(ctx, cam, env, npix, spp, mb, args.steps, args.warmup)
 
     # work counters of the same traversal on this rank's tile (instrumented launch, not timed)
     tile_pixels = D.tile_rows(npix, width, rank, world) * width
@@ -407,15 +414,31 @@ def main():
 
     frame_check = None
     if args.check and world > 1:
-        step()
-        finish_pending()
-        torch.cuda.synchronize()
+        _, _, frame = run_frames(ctx, cam, env, npix, spp, mb, 1, 0)
         if rank == 0:
             full = torch.empty(3 * npix, dtype=torch.float32, device="cuda")
             ctx.render_device(cam, env, npix, spp, mb, 0, 1, full.data_ptr(), stream.cuda_stream)
             torch.cuda.synchronize()
             frame_check = "bit-identical" if torch.equal(full.to(coll), frame) else "MISMATCH"
         dist.barrier()
+
+    # N > 1: the other BASELINE configs through the same multi-GPU path (row tiles + RCCL gather), so the
+    # driver's per-N runs measure every config's strong scaling, not only the headline's
+    multi_cfg = {}
+    if world > 1 and not args.no_extra and args.config == "C2":
+        for c, st, wu in (("C3", 2, 1), ("C4", 2, 1), ("C5", 1, 1)):
+            wlc = Wk.CONFIGS[c]
+            sc_c, cam_c, env_c, npix_c, spp_c, mb_c, ibl_c = wlc.inputs()
+            cc = make_ctx()
+            cc.set_scene(sc_c.V_p, sc_c.V_n, sc_c.V_uv, sc_c.faceData, sc_c.materialData, sc_c.BVH.exportArray)
+            cc.set_env(ibl_c)
+            el, kms, _ = run_frames(cc, cam_c, env_c, npix_c, spp_c, mb_c, st, wu)
+            cc.close()
+            multi_cfg[c] = {"workload": wlc.name, "value": round(npix_c * spp_c * st / el / 1e6, 3),
+                            "unit": "Msamples/s", "ms_per_step": round(el / st * 1e3, 3), "steps": st, "warmup": wu,
+                            "kernel_ms_max_rank": round(kms, 3),
+                            "parallelism": f"row-interleaved x{world}" + (" + gloo gather (one-GPU rehearsal)"
+                                                                          if rehearsal else " + RCCL gather")}
 
     if rank == 0:
         samples = npix * spp
@@ -434,6 +457,8 @@ def main():
         }
         if frame_check is not None:
             line["frame_check"] = f"gathered {world}-rank frame vs one-device render: {frame_check}"
+        if multi_cfg:
+            line["configs"] = multi_cfg
         if world == 1 and not args.no_extra:
             # the drop-in boundary's own rate: blocking rt_render into host memory (kernel + read-back),
             # same warmup / steps as the headline
