@@ -99,3 +99,50 @@ def test_scene_upload_waits_for_a_launch_in_flight(first, second, size):
     torch.cuda.synchronize()
     np.testing.assert_array_equal(a.cpu().numpy(), want)
     ctx.close()
+
+
+RCCL_ONE_RANK = r'''
+import os, sys
+sys.path.insert(0, sys.argv[1])
+import numpy as np
+import torch
+import torch.distributed as dist
+from ensem3a_openclraytracer_amd import _native
+from ensem3a_openclraytracer_amd import distributed as D
+from ensem3a_openclraytracer_amd import workloads as W
+os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=sys.argv[2], RANK="0", WORLD_SIZE="1")
+torch.cuda.set_device(0)
+dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+assert dist.get_backend() == "nccl"
+sc, cam, env, npix, spp, mb, ibl = W.PARITY_CASES["monkey_c3_64_s4"].inputs()
+ctx = _native.Context(device_ids=[0])
+ctx.set_scene(sc.V_p, sc.V_n, sc.V_uv, sc.faceData, sc.materialData, sc.BVH.exportArray)
+ctx.set_env(ibl)
+w = int(cam[6])
+tile = D.render_distributed(D.gpu_tile_renderer(ctx, cam, env, npix, spp, mb), npix, w, 0, 1, device="cuda",
+                            gather=False)
+bufs = [torch.empty_like(tile)]
+dist.gather(tile, gather_list=bufs, dst=0)   # RCCL
+frame = D.assemble(bufs, w, npix, 1)
+torch.cuda.synchronize()
+want = ctx.render(cam, env, npix, spp, mb)
+assert np.array_equal(frame.cpu().numpy(), want), "RCCL-gathered frame differs"
+ctx.close()
+dist.destroy_process_group()
+print("rccl ok")
+'''
+
+
+def test_rccl_gather_path_on_the_device():
+    """The multi-GPU path's collective on hardware: torch.distributed over RCCL ('nccl') with one rank,
+    the HIP tile renderer and the gather of distributed.render_distributed -- the frame equals the
+    direct render.  (Two ranks cannot share one GPU under RCCL; the 8-GPU run is the driver's.)"""
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    r = subprocess.run([sys.executable, "-c", RCCL_ONE_RANK, ROOT, str(port)], capture_output=True, text=True,
+                       timeout=240, env=env)
+    assert r.returncode == 0 and "rccl ok" in r.stdout, r.stdout[-2000:] + r.stderr[-3000:]
