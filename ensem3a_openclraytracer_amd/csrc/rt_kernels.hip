@@ -1186,7 +1186,6 @@ struct FastRay {
     int bt;           // best triangle's byte offset (48 t), -1 = none
     int brank;        // its rank in the reference DFS order
     bool any;         // any hit ends the ray (a shadow ray whose hit only matters as hit / miss)
-    int pend;         // deferred leaf (fast_step_defer), INT_MIN = none
 };
 
 // Returns true when the ray is already finished (no triangles / root box missed).
@@ -1199,7 +1198,6 @@ __device__ __forceinline__ bool fast_init(const DevScene& S, FastRay& R, rtm_f3 
     R.bt = -1;
     R.brank = -1;
     R.soff = 0;
-    R.pend = INT_MIN;
     if (S.ntri <= 0) return true;
     R.ix = 1.0f / d.x;
     R.iy = 1.0f / d.y;
@@ -1291,85 +1289,6 @@ __device__ __forceinline__ bool fast_step(const DevScene& S, FastRay& R, const c
         }
     }
     return true;
-}
-
-// ---- deferred leaves (build option RT_LEAF_DEFER = lanes): one step = one node for every tracing lane ----
-#ifndef RT_LEAF_DEFER
-#define RT_LEAF_DEFER 0
-#endif
-constexpr int kLeafDefer = RT_LEAF_DEFER;
-// In fast_step a wave's step runs the node code for its node lanes and the Moller-Trumbore code for
-// its leaf lanes, each with part of the lanes active (C3/C4: 0.33 of the lanes per VALU instruction).
-// Here a lane that meets a leaf parks it in one register (R.pend) and goes on with its next node; the
-// parked leaves of the wave are tested together once at least `thr` lanes hold one (their records
-// read by three loads), and a lane that has nothing left but its parked leaf tests it as an ordinary
-// item.  Culling may use an older best (less culling, never a different hit): the hit is the minimum
-// (k, rank) over accepted triangles, whatever their order.  Returns true when the ray is finished.
-template <bool COUNT, bool SOA, bool OVF>
-__device__ __forceinline__ bool fast_step_defer(FastRay& R, const char* nb, const char* tb, const LaneStack& st,
-                                                unsigned kstride, int thr, Cnt& c) {
-    auto test_leaf = [&](const float4& g0, const float4& g1, const float4& g2) __attribute__((always_inline)) {
-        if (COUNT) c.tris++;
-        float k;
-        int rank;
-        if (mt_vals(g0, g1, g2, R.o, R.d, &k, &rank) && k > 0.0001f && (k < R.bk || (k == R.bk && rank < R.brank))) {
-            R.bk = k;
-            R.bt = 48 * __float_as_int(g1.w);   // e1.w: the triangle's reference index
-            R.brank = rank;
-        }
-    };
-    // pop the next live entry; leaves go to the parking slot while it is free
-    auto next_item = [&]() __attribute__((always_inline)) {
-        while (R.soff > 0) {
-            R.soff -= st.stride;
-            const int2 en = st.template get<OVF>(R.soff);
-            if (__int_as_float(en.y) <= R.bk * CULL_MARGIN) {
-                if (en.x < 0 && R.pend == INT_MIN) {
-                    R.pend = en.x;
-                    continue;
-                }
-                R.item = en.x;
-                return;
-            }
-        }
-    };
-    if (R.item == INT_MIN && R.pend != INT_MIN) {   // nothing left but the parked leaf: test it now
-        R.item = R.pend;
-        R.pend = INT_MIN;
-    }
-    if (R.item != INT_MIN) {
-        const bool node = R.item >= 0;
-        const char* p = node ? nb + (SOA ? 16u : 16u * kNodeF4) * (unsigned)R.item : tb + ~(unsigned)R.item;
-        const unsigned ks = node ? kstride : 16u;
-        const float4 g0 = *reinterpret_cast<const float4*>(p);
-        const float4 g1 = *reinterpret_cast<const float4*>(p + ks);
-        const float4 g2 = *reinterpret_cast<const float4*>(p + 2 * ks);
-        const int2 e = *reinterpret_cast<const int2*>(p + (node ? 3 * ks : 0u));
-        if (COUNT) count_wave(c.wave_trav);
-        if (node) {
-            if (COUNT) { c.nodes++; c.boxes += 2; }
-            int next = node_pick<OVF>(g0, g1, g2, e, R.o, R.ix, R.iy, R.iz, R.bk * CULL_MARGIN, st, R.soff);
-            if (next < 0 && next != INT_MIN && R.pend == INT_MIN) {
-                R.pend = next;
-                next = INT_MIN;
-            }
-            R.item = next;
-        } else {
-            test_leaf(g0, g1, g2);
-            R.item = INT_MIN;
-        }
-        if (R.item == INT_MIN) next_item();
-    }
-    // the wave's parked leaves, tested together
-    if (__popcll(__ballot(R.pend != INT_MIN)) >= thr && R.pend != INT_MIN) {
-        if (COUNT) count_wave(c.wave_trav);
-        const char* p = tb + ~(unsigned)R.pend;
-        R.pend = INT_MIN;
-        test_leaf(*reinterpret_cast<const float4*>(p), *reinterpret_cast<const float4*>(p + 16),
-                  *reinterpret_cast<const float4*>(p + 32));
-    }
-    if (R.any && R.bt >= 0) return true;
-    return R.item == INT_MIN && R.pend == INT_MIN;
 }
 
 // ---- team traversal: TS lanes walk one ray (tiles with about one pixel per lane, option "walk_team") ----
@@ -1931,8 +1850,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WIDE ?
             if (tracing && (TS > 1 ? team_step<COUNT, SMEM, OVF>(TS, T, boff, nb, tb, lst, kstride, c)
                             : WIDE ? (STEP ? wide_step<COUNT, OVF>(T, wnb, wlb, lst, c)
                                            : wide_round<COUNT, OVF>(T, wnb, wlb, lst, c))
-                            : STEP ? (kLeafDefer > 0 ? fast_step_defer<COUNT, SMEM, OVF>(T, nb, tb, lst, kstride, kLeafDefer, c)
-                                                     : fast_step<COUNT, SMEM, OVF>(S, T, nb, tb, lst, kstride, c))
+                            : STEP ? fast_step<COUNT, SMEM, OVF>(S, T, nb, tb, lst, kstride, c)
                                    : fast_round<COUNT, SMEM, OVF>(S, T, nb, tb, lst, kstride, c)))
                 tracing = false;
             const unsigned long long tr = __ballot(tracing);
