@@ -1025,8 +1025,16 @@ hipError_t setup_pilot(rt_ctx* ctx, Device& d, rt::FrameParams& fp) {
     int k = ctx->pilot;
     if (k < 0) {   // auto: the tree walk on tiles of 1-16 pixels per resident lane (where the tail is long)
         const int64_t lanes = (int64_t)std::max(d.cus, 1) * 1280;
-        if (ctx->hs.nbrute > 0 || fp.spp < 16 || fp.nloc <= lanes || fp.nloc > 16 * lanes) return hipSuccess;
-        k = fp.spp / 8;
+        if (ctx->hs.nbrute > 0 || fp.spp < 16 || fp.nloc > 16 * lanes) return hipSuccess;
+        if (fp.nloc <= lanes) {
+            // small tiles (multi-GPU row tiles) of the BVH2 walk, whose pixels get teams of lanes
+            // (walk_team): the cost order starts the long chains first, pilot spp/16 (r03, 1/8 tiles:
+            // C3 62.6 -> 49.3 ms, C4 168 -> 142 ms; spp/8: 49.9 / 145.9)
+            if (use_wide(ctx) || fp.spp < 32) return hipSuccess;
+            k = fp.spp / 16;
+        } else {
+            k = fp.spp / 8;
+        }
     }
     if (k >= fp.spp) return hipSuccess;
     const size_t n = (size_t)fp.nloc;
