@@ -1025,12 +1025,15 @@ hipError_t setup_pilot(rt_ctx* ctx, Device& d, rt::FrameParams& fp) {
     int k = ctx->pilot;
     if (k < 0) {   // auto: the tree walk on tiles of 1-16 pixels per resident lane (where the tail is long)
         const int64_t lanes = (int64_t)std::max(d.cus, 1) * 1280;
-        if (ctx->hs.nbrute > 0 || fp.spp < 16 || fp.nloc > 16 * lanes) return hipSuccess;
+        // not on the 4-wide walk (C5), whose L2-missing walk loses the coherence of neighbouring pixels
+        // when they are reordered: r03 row tiles 1/2, 1/4, 1/8: 3,005 / 1,626 / 937 ms without the pilot,
+        // 3,185 / 1,694 / 938 with it
+        if (ctx->hs.nbrute > 0 || use_wide(ctx) || fp.spp < 16 || fp.nloc > 16 * lanes) return hipSuccess;
         if (fp.nloc <= lanes) {
             // small tiles (multi-GPU row tiles) of the BVH2 walk, whose pixels get teams of lanes
             // (walk_team): the cost order starts the long chains first, pilot spp/16 (r03, 1/8 tiles:
             // C3 62.6 -> 49.3 ms, C4 168 -> 142 ms; spp/8: 49.9 / 145.9)
-            if (use_wide(ctx) || fp.spp < 32) return hipSuccess;
+            if (fp.spp < 32) return hipSuccess;
             k = fp.spp / 16;
         } else {
             k = fp.spp / 8;
