@@ -1623,6 +1623,17 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WIDE ?
     int s = 0;
     bool drew = false;   // the current sample has drawn random numbers (a diffuse or glossy bounce)
     int cost = 0;        // pass 1: rays this pixel traced (pilot_cost)
+    // The deterministic prefix of the pixel's samples (FrameParams::fixed_point; BVH2 walk): a sample's
+    // path up to its first diffuse or glossy bounce draws no random number -- it is the cached camera
+    // hit followed by straight-through glass bounces (Raytracing.cl:72-77) -- so it is the same path in
+    // every sample of the pixel.  The state at the first bounce that draws (bounce j, surface, sample
+    // colour so far, and the ray that reached it) is kept once met, and every later sample of the
+    // pixel starts there instead of re-tracing the glass chain: the same rays would give the same hits.
+    constexpr bool PREFIX = !WIDE;
+    bool pre = false;
+    int pre_j = 0, pre_tri = -1;
+    rtm_f3 pre_so = rtm_v3(1, 1, 1), pre_o = rtm_v3(0, 0, 0), pre_d = rtm_v3(0, 0, 1);
+    float pre_k = 1000.0f;
 
     auto write_pixel = [&]() __attribute__((always_inline)) {
         if (team_leader) store_pixel(out, p, acc, spp);
@@ -1651,6 +1662,11 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WIDE ?
         tri = tc; j = 0;
         so = rtm_v3(1, 1, 1);
         drew = false;
+        if (PREFIX && pre) {   // the next sample starts after the deterministic prefix
+            tri = pre_tri; j = pre_j;
+            so = pre_so;
+            T.o = pre_o; T.d = pre_d; T.bk = pre_k;
+        }
     };
     // A sample that drew no random numbers (camera ray escaped or on an emitter, or only glass
     // bounces): the RNG state is unchanged, so every later sample of the pixel is this sample again.
@@ -1696,6 +1712,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WIDE ?
                     acc = rtm_v3(0, 0, 0);
                     s = 0;
                     cost = 0;
+                    pre = false;
                     phase = PRIMARY;
                     logme = LOG && i == F.log_pixel;
                     if (F.pass == 2) {   // continue from the pilot state: camera hit cached, sample s next
@@ -1813,6 +1830,12 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WIDE ?
                         float invPdf = 0.0f;
                         rtm_f3 brdf = rtm_v3(0, 0, 0);
                         if (COUNT) count_event(c, cm.type);
+                        if (PREFIX && F.fixed_point && cm.type != 3 && !drew && j > 0 && !pre && !(LOG && logme)) {
+                            pre = true;   // the first bounce of the sample that draws, reached through glass only
+                            pre_j = j; pre_tri = tri;
+                            pre_so = so;
+                            pre_o = T.o; pre_d = T.d; pre_k = T.bk;
+                        }
                         drew = drew || cm.type != 3;
                         if (cm.type != 3) {   // diffuse (1) or glossy (2): one sampler stream for both
                             Bd = hemi_sample(cm.type == 1, n, S.tri_frame[3 * tri], S.tri_frame[3 * tri + 1], f2,

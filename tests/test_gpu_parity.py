@@ -394,6 +394,34 @@ def test_team_walk_row_tiles_full_width(kl, config, spp):
         np.testing.assert_array_equal(frames[0], f)
 
 
+@pytest.mark.parametrize("config,row0,step,spp", [("C4", 1, 4, 64), ("C3", 5, 8, 64), ("C3", 0, 2, 32)])
+def test_auto_tile_schedules_render_identically(kl, config, row0, step, spp):
+    """Row tiles with every schedule option on auto -- a pilot pass, pass 2 in cost order with the team
+    size chosen on the device from the pixels pass 1 left (C4 1/4 tile: teams of 4; C3 1/2 tile: one
+    lane), or a small-tile pilot with teams in both passes (C3 1/8 tile) -- against one lane per pixel
+    in one pass: bit for bit."""
+    import torch
+    from ensem3a_openclraytracer_amd import distributed as D
+    sc, cam, env, npix, _, mb, ibl = W.CONFIGS[config].inputs()
+    _launch(kl, sc, cam, env, npix, 1, mb, ibl, "fast")   # uploads the scene and IBL
+    ctx = kl.native
+    width = int(cam[6])
+    rows = D.tile_rows(npix, width, row0, step)
+    out = torch.empty(3 * width * rows, dtype=torch.float32, device="cuda")
+    frames = []
+    try:
+        for opts in ({}, {"walk_team": 1, "pilot": 0}):
+            for k, v in opts.items():
+                ctx.set_option(k, v)
+            ctx.render_device(cam, env, npix, spp, mb, row0, step, out.data_ptr())
+            torch.cuda.synchronize()
+            frames.append(out.cpu().numpy().copy())
+    finally:
+        ctx.set_option("walk_team", 0)
+        ctx.set_option("pilot", -1)
+    np.testing.assert_array_equal(frames[0], frames[1])
+
+
 @pytest.mark.parametrize("case", ["cornell_64_s4", "monkey_c3_64_s4"])
 def test_resident_wave_cap_renders_identically(kl, case):
     """waves (cap on resident waves per SIMD of the persistent grid) changes which wave renders which
