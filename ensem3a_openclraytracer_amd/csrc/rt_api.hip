@@ -104,6 +104,7 @@ struct rt_ctx {
     int block = 128;
     int bvh_width = 0;  // FAST tree walk: 2 = BVH2 nodes, 4 = the 4-wide quantised layout, 0 = auto (option "bvh_width")
     int fixed_point = 1;  // sum the repeats of a sample that draws no random number (FrameParams::fixed_point)
+    int sun_cache = 1;    // trace the first drawing bounce's shadow ray once per pixel (FrameParams::sun_cache)
     int pilot = -1;       // two-pass launches: pilot samples per pixel (0 = one pass, -1 = auto; FrameParams::pilot)
     int pilot_chunk = 0;  // pixels ordered together (0 = auto: 64 brute force, 1 tree walk)
     int pilot_levels = 0; // cost bins of the order (0 = auto: 256)
@@ -679,6 +680,7 @@ int check_frame(rt_ctx* ctx, const float* cam, const float* env, int64_t npix, i
     fp->sun_any = (ctx->sun_any && !ctx->hs.has_glass) ? 1 : 0;
     fp->wide = use_wide(ctx) ? 1 : 0;
     fp->fixed_point = ctx->fixed_point;
+    fp->sun_cache = ctx->fixed_point && ctx->sun_cache ? 1 : 0;
     fp->pass = 0;
     fp->pilot = 0;
     fp->pilot_chunk = 1;
@@ -854,6 +856,11 @@ int rt_set_option(rt_ctx* ctx, const char* key, int64_t value) {
         if (value != 0 && (value < kStackLdsMin || value > rt::kStackLds))
             return set_err(ctx, RT_ERR_ARG, "stack_lds must be 0 (auto) or %d..%d", kStackLdsMin, rt::kStackLds);
         ctx->stack_lds = (int)value;
+        return RT_OK;
+    }
+    if (!std::strcmp(key, "sun_cache")) {
+        if (value != 0 && value != 1) return set_err(ctx, RT_ERR_ARG, "sun_cache must be 0 or 1");
+        ctx->sun_cache = (int)value;
         return RT_OK;
     }
     if (!std::strcmp(key, "fixed_point")) {

@@ -114,6 +114,9 @@ struct FrameParams {
     // a sample that draws no random number (it ends at its first loop head: camera ray escaped or
     // on an emitter) is every later sample of its pixel: the rest are summed without re-running it
     int32_t fixed_point;
+    // the shadow ray of a sample's first diffuse or glossy bounce leaves from the same point towards
+    // the same sun in every sample of the pixel: traced once, its hit kept (implies fixed_point)
+    int32_t sun_cache;
     // Two-pass launches (launch_render, option "pilot"): pass 1 renders the first `pilot` samples of
     // every pixel and saves each unfinished pixel's state (pilot_state: acc.xyz | kc, seed0 seed1 tc s)
     // and the rays it traced (pilot_cost); the pixels are then ordered by that cost, most first

@@ -947,6 +947,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) r
     rtm_f3 acc = rtm_v3(0, 0, 0);
     int s = 0;
     int cost = 0;   // pass 1: rays this pixel traced (pilot_cost)
+    int sun0 = -2;  // the first bounce's shadow-ray hit (-1 = miss; -2 = not traced yet)
 
     // pass 1 (FrameParams::pass): after the pilot samples, save the pixel's state for pass 2; the
     // pixel is written (and its cost set to 0) when all its samples are done
@@ -980,6 +981,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) r
                     acc = rtm_v3(0, 0, 0);
                     s = 0;
                     cost = 0;
+                    sun0 = -2;
                     phase = PRIMARY;
                     logme = LOG && i == F.log_pixel;
                     if (F.pass == 2) {   // continue from the pilot state: camera hit cached, sample s next
@@ -1099,6 +1101,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) r
             log_event(F, phase == BOUNCE ? 1.0f : 2.0f, j, Bo, td, h.tri >= 0 ? h.k : -1.0f, hm, so);
         }
         int sun_hit = -2;   // the shadow ray's hit for the sun term below (-1 = miss; -2 = no sun term now)
+        // the first bounce leaves from the cached camera hit in every sample of the pixel, so its shadow
+        // ray towards the sun is the same ray each time: traced once per pixel (FrameParams::fixed_point)
+        const bool sun_first = TRAV == TRAV_FAST && F.sun_cache && j == 0 && !(LOG && logme);
         if (phase == BOUNCE) {
             if (h.tri >= 0) {
                 tri = h.tri; k = h.k;
@@ -1117,11 +1122,14 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) r
                 }
             } else if (TRAV == TRAV_FAST && F.sun_skip) {
                 sun_hit = -1;   // unlit sun: the shadow ray cannot change the sample (FrameParams::sun_skip)
+            } else if (sun_first && sun0 != -2) {
+                sun_hit = sun0;   // the first bounce's shadow ray, traced in an earlier sample of the pixel
             } else {
                 phase = SUN;
             }
         } else {
             sun_hit = h.tri;
+            if (sun_first) sun0 = h.tri;
         }
         if (sun_hit != -2) {  // SUN (Raytracing.cl:115-137)
             rtm_f3 sunLight = rtm_v3(0, 0, 0);
@@ -1634,6 +1642,13 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WIDE ?
     int pre_j = 0, pre_tri = -1;
     rtm_f3 pre_so = rtm_v3(1, 1, 1), pre_o = rtm_v3(0, 0, 0), pre_d = rtm_v3(0, 0, 1);
     float pre_k = 1000.0f;
+    // The sample's first diffuse or glossy bounce leaves from the same point in every sample (the end of
+    // the deterministic prefix), so when its bounce ray escapes, the shadow ray towards the sun
+    // (Raytracing.cl:115-124) is the same ray in every sample: its hit is traced once per pixel and kept.
+    constexpr bool SUNC = !WIDE;
+    constexpr int SUN_UNKNOWN = -2;
+    int sun_c = SUN_UNKNOWN;   // the first drawing bounce's shadow-ray hit (triangle, -1 for none)
+    bool fdb = false;          // the bounce in flight is the sample's first drawing bounce
 
     auto write_pixel = [&]() __attribute__((always_inline)) {
         if (team_leader) store_pixel(out, p, acc, spp);
@@ -1713,6 +1728,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WIDE ?
                     s = 0;
                     cost = 0;
                     pre = false;
+                    sun_c = SUN_UNKNOWN;
                     phase = PRIMARY;
                     logme = LOG && i == F.log_pixel;
                     if (F.pass == 2) {   // continue from the pilot state: camera hit cached, sample s next
@@ -1741,7 +1757,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WIDE ?
 
         // -- advance every lane without a ray in flight until it needs one --
         if (!tracing && phase != DONE && phase != FETCH) {
-            const Hit h{T.bk, T.bt >= 0 ? (int)((unsigned)T.bt / 48u) : -1};
+            Hit h{T.bk, T.bt >= 0 ? (int)((unsigned)T.bt / 48u) : -1};
             if (phase == PRIMARY) {
                 tc = h.tri;
                 kc = h.k;
@@ -1779,7 +1795,10 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WIDE ?
                     phase = SUN;   // escaped: shadow ray towards the sun (Raytracing.cl:115-124)
                     // unlit sun (FrameParams::sun_skip): the shadow ray cannot change the sample; it is not
                     // traced and the sun term below runs now with h, the bounce ray's miss
-                    if (!F.sun_skip) {
+                    if (F.sun_skip) {
+                    } else if (SUNC && fdb && sun_c != SUN_UNKNOWN) {
+                        h.tri = sun_c;   // the first drawing bounce's shadow ray, traced in an earlier sample
+                    } else {
                         start(T.o, C.sun);
                         T.any = F.sun_any != 0;
                         if (!tracing) continue;  // unreachable in practice (root box always hit from inside)
@@ -1793,6 +1812,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WIDE ?
                 }
                 rtm_f3 sunLight = rtm_v3(0, 0, 0);
                 if (COUNT) c.sun++;
+                if (SUNC && fdb) sun_c = h.tri;
                 const Mat cm = load_mat(S.mat, __float_as_int(S.tri_shade[tri].w));
                 if (h.tri < 0 && cm.type != 3) sunLight = rtm_v3(e3, e3, e3);
                 if (h.tri >= 0) {
@@ -1836,6 +1856,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WIDE ?
                             pre_so = so;
                             pre_o = T.o; pre_d = T.d; pre_k = T.bk;
                         }
+                        fdb = SUNC && F.sun_cache && cm.type != 3 && !drew && !F.sun_skip && !(LOG && logme);
                         drew = drew || cm.type != 3;
                         if (cm.type != 3) {   // diffuse (1) or glossy (2): one sampler stream for both
                             Bd = hemi_sample(cm.type == 1, n, S.tri_frame[3 * tri], S.tri_frame[3 * tri + 1], f2,

@@ -88,7 +88,7 @@ int rt_set_env(rt_ctx* ctx, const uint8_t* rgba, int w, int h);
  * same hits), "waves" (persistent grid: at most this many waves per SIMD, 0 =
  * occupancy limit), "block" (threads per block: 64, 128 or 256), and the
  * tuning switches documented in DESIGN.md 4.2 ("sun_skip", "sun_any",
- * "fixed_point", "pilot", "pilot_chunk", "pilot_levels", "stack_lds",
+ * "fixed_point", "sun_cache", "pilot", "pilot_chunk", "pilot_levels", "stack_lds",
  * "bvh_width"): every option renders the same frame.
  * "bvh" and "brute_max" may be changed after rt_set_scene. */
 int rt_set_option(rt_ctx* ctx, const char* key, int64_t value);

@@ -879,6 +879,30 @@ def test_fixed_point_samples_render_identically(kl, case):
         kl.native.set_option("fixed_point", 2)
 
 
+@pytest.mark.parametrize("case", ["serre_96x54_s4", "cornell_128_s16", "monkey_c3_64_s4", "serre_sky_s64"])
+def test_sun_cache_renders_identically(kl, case):
+    """sun_cache: the shadow ray of a sample's first diffuse or glossy bounce leaves from the end of the
+    pixel's deterministic prefix towards the sun, the same ray in every sample; it is traced once per
+    pixel and its hit kept.  Same frame with it off and against the oracle, on the lock-step kernel
+    (cornell: lit sun, no glass) and the tree walk (serre: glass and a lit sun), fewer rays traced."""
+    spp_over = None
+    if case == "serre_sky_s64":
+        case, spp_over = "serre_96x54_s4", 64
+    sc, cam, env, npix, spp, mb, ibl = W.PARITY_CASES[case].inputs()
+    spp = spp_over or spp
+    try:
+        kl.native.set_option("sun_cache", 0)
+        full = _launch(kl, sc, cam, env, npix, spp, mb, ibl, "fast")
+        kl.native.set_option("sun_cache", 1)
+        fast = _launch(kl, sc, cam, env, npix, spp, mb, ibl, "fast")
+    finally:
+        kl.native.set_option("sun_cache", 1)
+    np.testing.assert_array_equal(fast, full)
+    np.testing.assert_array_equal(fast, _oracle(sc, cam, env, npix, spp, mb, ibl))
+    with pytest.raises(_native.NativeError, match="sun_cache"):
+        kl.native.set_option("sun_cache", 2)
+
+
 @pytest.mark.parametrize("case,pilot", [("cornell_128_s16", 4), ("cornell_128_s16", 1), ("monkey_c3_64_s4", 2),
                                         ("serre_96x54_s4", 3), ("proto_64_s4", 1)])
 def test_two_pass_pilot_renders_identically(kl, case, pilot):
