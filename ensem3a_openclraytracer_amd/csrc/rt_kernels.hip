@@ -1645,7 +1645,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WIDE ?
     // The sample's first diffuse or glossy bounce leaves from the same point in every sample (the end of
     // the deterministic prefix), so when its bounce ray escapes, the shadow ray towards the sun
     // (Raytracing.cl:115-124) is the same ray in every sample: its hit is traced once per pixel and kept.
-    constexpr bool SUNC = !WIDE;
+    constexpr bool SUNC = true;
     constexpr int SUN_UNKNOWN = -2;
     int sun_c = SUN_UNKNOWN;   // the first drawing bounce's shadow-ray hit (triangle, -1 for none)
     bool fdb = false;          // the bounce in flight is the sample's first drawing bounce
