@@ -7,7 +7,7 @@ the chain where it lands on a computed offset (trails merge once they share an o
 the frame bit-identical.  This script measures, per sampled pixel, the chain latency in traced
 rays for T = 1..4 with G_t = t * spp / T * mu (static guesses), against the serial chain.
 
-    python tools/chain_speculation.py [CONFIG] [PIXELS] [MU]
+    python tools/chain_speculation.py [CONFIG] [PIXELS] [MU]   (MU 0: per pixel, from a spp/8 pilot)
 """
 import ctypes
 import heapq
@@ -46,6 +46,12 @@ def chain(nd, spp):
             break
         D += nd[D // 2]
     return seq
+
+
+def pilot_mu(nd, spp, k):
+    """Draws per sample over the chain's first k samples (what a pilot pass of k samples knows)."""
+    seq = chain(nd, k + 1)
+    return max(seq[-1] / k, 2.0)
 
 
 def speculate(nd, nr, spp, T, mu):
@@ -108,7 +114,8 @@ def main():
     print(f"{name}: {npx} pixels, draws/sample mean {mus.mean():.2f} (std {mus.std():.2f}); serial chain "
           f"mean {ser.mean():.1f} rays, max {ser.max()}")
     for T in (2, 3, 4):
-        r = [speculate(nd, nr, spp, T, mu) for _, _, nd, nr in tr]
+        r = [speculate(nd, nr, spp, T, mu if mu > 0 else pilot_mu(nd, spp, max(spp // 8, 1)))
+             for _, _, nd, nr in tr]
         lat = np.array([a for a, _ in r], float)
         wk = np.array([b for _, b in r], float)
         print(f"T={T}: latency mean {lat.mean():.1f} p99 {np.percentile(lat, 99):.1f} max {lat.max():.0f} rays "
