@@ -207,8 +207,28 @@ __device__ __forceinline__ bool mt_vals(float4 g0, float4 g1, float4 g2, rtm_f3 
 // A lane's FAST traversal stack: entries below cap bytes in LDS ([entry][blockDim]
 // int2, conflict-free), deeper ones in the HBM overflow buffer ([entry][lanes]).
 // off = entry index * stride (bytes of LDS between a lane's entries).
+#ifndef RT_STACK_AS
+#define RT_STACK_AS 1
+#endif
+#if RT_STACK_AS
+// The LDS part is addressed through an LDS-qualified pointer: the compiler then cannot merge the
+// LDS and overflow branches of put/get into one generic (flat) access, which waits on both the
+// vector-memory and the LDS counters
+typedef char __attribute__((address_space(3))) lds_char;
+typedef unsigned long long __attribute__((address_space(3))) lds_u64;
+#else
+typedef char lds_char;
+typedef unsigned long long lds_u64;
+#endif
+// a stack entry (ref, entry distance bits) as one 64-bit LDS word
+__device__ __forceinline__ unsigned long long pack_entry(int2 e) {
+    return ((unsigned long long)(unsigned)e.y << 32) | (unsigned)e.x;
+}
+__device__ __forceinline__ int2 unpack_entry(unsigned long long v) {
+    return make_int2((int)(unsigned)v, (int)(unsigned)(v >> 32));
+}
 struct LaneStack {
-    char* lds;                       // per lane
+    lds_char* lds;                   // per lane
     int2* ovf;                       // uniform base; the lane's slot is added only on the rare spill path
     unsigned stride, cap, shift, ostride;
     __device__ __forceinline__ unsigned slot(unsigned off) const {
@@ -217,13 +237,13 @@ struct LaneStack {
     // OVF = false: the whole stack fits in LDS (stack_lds == depth) and no spill code is emitted
     template <bool OVF>
     __device__ __forceinline__ void put(unsigned off, int2 e) const {
-        if (!OVF || off < cap) *reinterpret_cast<int2*>(lds + off) = e;
+        if (!OVF || off < cap) *(lds_u64*)(lds + off) = pack_entry(e);
         else ovf[slot(off)] = e;
     }
     template <bool OVF>
     __device__ __forceinline__ int2 get(unsigned off) const {
         int2 e;
-        if (!OVF || off < cap) e = *reinterpret_cast<const int2*>(lds + off);
+        if (!OVF || off < cap) e = unpack_entry(*(const lds_u64*)(lds + off));
         else e = ovf[slot(off)];
         return e;
     }
@@ -231,7 +251,7 @@ struct LaneStack {
     template <bool OVF>
     __device__ __forceinline__ int2 get_lane(unsigned off, int dl) const {
         int2 e;
-        if (!OVF || off < cap) e = *reinterpret_cast<const int2*>(lds + off + 8 * dl);
+        if (!OVF || off < cap) e = unpack_entry(*(const lds_u64*)(lds + off + 8 * dl));
         else e = ovf[(unsigned)((int)slot(off) + dl)];
         return e;
     }
@@ -240,7 +260,7 @@ struct LaneStack {
 __device__ __forceinline__ LaneStack lane_stack(const DevScene& S, int* lds_base) {
     LaneStack st;
     const unsigned B = blockDim.x;
-    st.lds = reinterpret_cast<char*>(lds_base) + 8 * threadIdx.x;
+    st.lds = (lds_char*)(reinterpret_cast<char*>(lds_base)) + 8 * threadIdx.x;
     st.stride = 8u * B;
     st.cap = (unsigned)S.stack_lds * st.stride;
     st.shift = (unsigned)__builtin_ctz(st.stride);
@@ -1422,6 +1442,10 @@ __device__ __forceinline__ bool team_step(int ts, FastRay& R, unsigned& boff, co
 // k > 1e-4, lowest (k, rank)), so the hit is the same.  Returns true when the ray is finished.
 // The wide node on its loaded data: the hit children sorted by entry distance, the others pushed
 // farthest first.  Returns the nearest hit child, or INT_MIN (pop next).
+#ifndef RT_WIDE_PK
+#define RT_WIDE_PK 0
+#endif
+typedef float f2 __attribute__((ext_vector_type(2)));
 template <bool COUNT, bool OVF>
 __device__ __forceinline__ int wide_node(float4 g0, float4 g1, float4 g2, float4 g3, FastRay& R, const LaneStack& st,
                                          Cnt& c) {
@@ -1434,6 +1458,26 @@ __device__ __forceinline__ int wide_node(float4 g0, float4 g1, float4 g2, float4
     const unsigned qhx = __float_as_uint(g2.w), qhy = __float_as_uint(g3.x), qhz = __float_as_uint(g3.y);
     int r[4] = {__float_as_int(g1.x), __float_as_int(g1.y), __float_as_int(g1.z), __float_as_int(g1.w)};
     float t[4];
+#if RT_WIDE_PK
+    // the (lo, hi) pair of each axis in one packed-FP32 lane pair: v_pk_fma / v_pk_add / v_pk_mul
+    // round each element exactly like the scalar fma / sub / mul below
+    const f2 px = {g0.x, g0.x}, py = {g0.y, g0.y}, pz = {g0.z, g0.z};
+    const f2 sxx = {sx, sx}, syy = {sy, sy}, szz = {sz, sz};
+    const f2 nox = {-R.o.x, -R.o.x}, noy = {-R.o.y, -R.o.y}, noz = {-R.o.z, -R.o.z};
+    const f2 ixx = {R.ix, R.ix}, iyy = {R.iy, R.iy}, izz = {R.iz, R.iz};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        auto qq = [&](unsigned wl, unsigned wh) -> f2 {
+            return f2{(float)((wl >> (8 * i)) & 255u), (float)((wh >> (8 * i)) & 255u)};
+        };
+        const f2 tx = (__builtin_elementwise_fma(qq(qlx, qhx), sxx, px) + nox) * ixx;
+        const f2 ty = (__builtin_elementwise_fma(qq(qly, qhy), syy, py) + noy) * iyy;
+        const f2 tz = (__builtin_elementwise_fma(qq(qlz, qhz), szz, pz) + noz) * izz;
+        const float tn = fmaxf(fmaxf(fminf(tx.x, tx.y), fminf(ty.x, ty.y)), fminf(tz.x, tz.y));
+        const float tm = fminf(fminf(fmaxf(tx.x, tx.y), fmaxf(ty.x, ty.y)), fmaxf(tz.x, tz.y));
+        t[i] = (r[i] != INT_MIN && box_hit(tn, tm, cull)) ? tn : INFINITY;   // misses sort last
+    }
+#else
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
         // p + q * s with q * s exact (s a power of two, q < 256): one correctly rounded fma gives the
@@ -1444,6 +1488,7 @@ __device__ __forceinline__ int wide_node(float4 g0, float4 g1, float4 g2, float4
              dq(g0.z, qhz, sz), R.o, R.ix, R.iy, R.iz, tn, tx);
         t[i] = (r[i] != INT_MIN && box_hit(tn, tx, cull)) ? tn : INFINITY;   // misses sort last
     }
+#endif
     if (COUNT) {
         c.nodes++;
         c.boxes += (r[0] != INT_MIN) + (r[1] != INT_MIN) + (r[2] != INT_MIN) + (r[3] != INT_MIN);
