@@ -1275,6 +1275,19 @@ __device__ __forceinline__ bool fast_round(const DevScene& S, FastRay& R, const 
     return true;
 }
 
+// The fourth load of an item step reads a node's child refs, and for a leaf the last 8 bytes of its
+// record (e2.z and the pad), whose e2.z the leaf test takes from it: both kinds of lanes then use the
+// load, so the compiler issues it with the other three before the node / leaf branch instead of
+// sinking it into the node branch, where a wave holding both kinds waited for it after the leaf code
+// (a second memory round trip per step).
+constexpr unsigned kLeafTail = 40u;
+#ifndef RT_FLAT_STEP
+#define RT_FLAT_STEP 1
+#endif
+__device__ __forceinline__ float4 leaf_e2(float4 g2, int2 tail) {
+    return make_float4(g2.x, g2.y, __int_as_float(tail.x), g2.w);
+}
+
 // One item of trace_fast's loop per call: an internal node or a leaf, then a pop when the item
 // yields no next item.  The per-lane sequence of node steps, leaf tests and pops is trace_fast's, so
 // the hit is the same.  Every tracing lane fetches its item with the SAME four vector loads, whether
@@ -1291,8 +1304,41 @@ __device__ __forceinline__ bool fast_step(const DevScene& S, FastRay& R, const c
     const float4 g0 = *reinterpret_cast<const float4*>(p);
     const float4 g1 = *reinterpret_cast<const float4*>(p + ks);
     const float4 g2 = *reinterpret_cast<const float4*>(p + 2 * ks);
-    const int2 e = *reinterpret_cast<const int2*>(p + (node ? 3 * ks : 0u));
+    const int2 e = *reinterpret_cast<const int2*>(p + (node ? 3 * ks : kLeafTail));
     if (COUNT) count_wave(c.wave_trav);
+#if RT_FLAT_STEP
+    // Both tests on every lane's item, outcomes by selects: a wave's step almost always holds node
+    // and leaf lanes together (C3: ~20 % of the items are leaves, ~40 lanes trace), so both codes run
+    // anyway; in one basic block the compiler can sink no load into one kind's branch.  The node
+    // arithmetic on a leaf record and the Moller-Trumbore arithmetic on a node record are discarded.
+    const float cull = R.bk * CULL_MARGIN;
+    float t0n, t0x, t1n, t1x;
+    slab(g0.x, g0.y, g0.z, g0.w, g2.x, g2.y, R.o, R.ix, R.iy, R.iz, t0n, t0x);
+    slab(g1.x, g1.y, g1.z, g1.w, g2.z, g2.w, R.o, R.ix, R.iy, R.iz, t1n, t1x);
+    const bool h0 = node && box_hit(t0n, t0x, cull), h1 = node && box_hit(t1n, t1x, cull);
+    float k;
+    int rank;
+    const bool mt = mt_vals(g0, g1, leaf_e2(g2, e), R.o, R.d, &k, &rank);
+    const bool take = !node && mt && k > 0.0001f && (k < R.bk || (k == R.bk && rank < R.brank));
+    if (COUNT) {
+        if (node) { c.nodes++; c.boxes += 2; }
+        else c.tris++;
+    }
+    R.bk = take ? k : R.bk;
+    R.bt = take ? 48 * __float_as_int(g1.w) : R.bt;   // e1.w: the triangle's reference index
+    R.brank = take ? rank : R.brank;
+    const bool first0 = t0n <= t1n;
+    if (h0 && h1) {   // the farther child waits on the stack
+        st.template put<OVF>(R.soff, make_int2(first0 ? e.y : e.x, __float_as_int(first0 ? t1n : t0n)));
+        R.soff += st.stride;
+    }
+    const int next = (h0 && h1) ? (first0 ? e.x : e.y) : h0 ? e.x : h1 ? e.y : INT_MIN;
+    if (take && R.any) return true;
+    if (next != INT_MIN) {
+        R.item = next;
+        return false;
+    }
+#else
     if (node) {
         if (COUNT) { c.nodes++; c.boxes += 2; }
         R.item = node_pick<OVF>(g0, g1, g2, e, R.o, R.ix, R.iy, R.iz, R.bk * CULL_MARGIN, st, R.soff);
@@ -1301,13 +1347,14 @@ __device__ __forceinline__ bool fast_step(const DevScene& S, FastRay& R, const c
         if (COUNT) c.tris++;
         float k;
         int rank;
-        if (mt_vals(g0, g1, g2, R.o, R.d, &k, &rank) && k > 0.0001f && (k < R.bk || (k == R.bk && rank < R.brank))) {
+        if (mt_vals(g0, g1, leaf_e2(g2, e), R.o, R.d, &k, &rank) && k > 0.0001f && (k < R.bk || (k == R.bk && rank < R.brank))) {
             R.bk = k;
             R.bt = 48 * __float_as_int(g1.w);   // e1.w: the triangle's reference index
             R.brank = rank;
             if (R.any) return true;
         }
     }
+#endif
     while (R.soff > 0) {   // pop the next item still in front of the best hit
         R.soff -= st.stride;
         const int2 en = st.template get<OVF>(R.soff);
@@ -1395,7 +1442,32 @@ __device__ __forceinline__ bool team_step(int ts, FastRay& R, unsigned& boff, co
         const float4 g0 = *reinterpret_cast<const float4*>(p);
         const float4 g1 = *reinterpret_cast<const float4*>(p + ks);
         const float4 g2 = *reinterpret_cast<const float4*>(p + 2 * ks);
-        const int2 e = *reinterpret_cast<const int2*>(p + (node ? 3 * ks : 0u));
+        const int2 e = *reinterpret_cast<const int2*>(p + (node ? 3 * ks : kLeafTail));
+#if RT_FLAT_STEP
+        // both tests, outcomes by selects (fast_step)
+        const float cull = R.bk * CULL_MARGIN;
+        float t0n, t0x, t1n, t1x;
+        slab(g0.x, g0.y, g0.z, g0.w, g2.x, g2.y, R.o, R.ix, R.iy, R.iz, t0n, t0x);
+        slab(g1.x, g1.y, g1.z, g1.w, g2.z, g2.w, R.o, R.ix, R.iy, R.iz, t1n, t1x);
+        const bool h0 = node && box_hit(t0n, t0x, cull), h1 = node && box_hit(t1n, t1x, cull);
+        float k;
+        int rank;
+        const bool mt = mt_vals(g0, g1, leaf_e2(g2, e), R.o, R.d, &k, &rank);
+        improved = !node && mt && k > 0.0001f && (k < R.bk || (k == R.bk && rank < R.brank));
+        if (COUNT) {
+            if (node) { c.nodes++; c.boxes += 2; }
+            else c.tris++;
+        }
+        R.bk = improved ? k : R.bk;
+        R.bt = improved ? 48 * __float_as_int(g1.w) : R.bt;
+        R.brank = improved ? rank : R.brank;
+        const bool first0 = t0n <= t1n;
+        if (h0 && h1) {
+            st.template put<OVF>(R.soff, make_int2(first0 ? e.y : e.x, __float_as_int(first0 ? t1n : t0n)));
+            R.soff += st.stride;
+        }
+        R.item = (h0 && h1) ? (first0 ? e.x : e.y) : h0 ? e.x : h1 ? e.y : NO_ITEM;
+#else
         if (node) {
             if (COUNT) { c.nodes++; c.boxes += 2; }
             R.item = node_pick<OVF>(g0, g1, g2, e, R.o, R.ix, R.iy, R.iz, R.bk * CULL_MARGIN, st, R.soff);
@@ -1403,7 +1475,7 @@ __device__ __forceinline__ bool team_step(int ts, FastRay& R, unsigned& boff, co
             if (COUNT) c.tris++;
             float k;
             int rank;
-            if (mt_vals(g0, g1, g2, R.o, R.d, &k, &rank) && k > 0.0001f &&
+            if (mt_vals(g0, g1, leaf_e2(g2, e), R.o, R.d, &k, &rank) && k > 0.0001f &&
                 (k < R.bk || (k == R.bk && rank < R.brank))) {
                 R.bk = k;
                 R.bt = 48 * __float_as_int(g1.w);
@@ -1412,6 +1484,7 @@ __device__ __forceinline__ bool team_step(int ts, FastRay& R, unsigned& boff, co
             }
             R.item = NO_ITEM;
         }
+#endif
     }
     if (COUNT) count_wave(c.wave_trav);
     // 4. the team's best: lowest (k, rank) over the team, in every lane
