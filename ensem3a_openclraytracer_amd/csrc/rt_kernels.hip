@@ -1515,13 +1515,16 @@ __device__ __forceinline__ bool team_step(int ts, FastRay& R, unsigned& boff, co
 // k > 1e-4, lowest (k, rank)), so the hit is the same.  Returns true when the ray is finished.
 // The wide node on its loaded data: the hit children sorted by entry distance, the others pushed
 // farthest first.  Returns the nearest hit child, or INT_MIN (pop next).
+#ifndef RT_FLAT_WIDE
+#define RT_FLAT_WIDE 1
+#endif
 #ifndef RT_WIDE_PK
 #define RT_WIDE_PK 0
 #endif
 typedef float f2 __attribute__((ext_vector_type(2)));
 template <bool COUNT, bool OVF>
 __device__ __forceinline__ int wide_node(float4 g0, float4 g1, float4 g2, float4 g3, FastRay& R, const LaneStack& st,
-                                         Cnt& c) {
+                                         Cnt& c, bool on = true) {   // on = false: no child is hit
     const float cull = R.bk * CULL_MARGIN;
     const unsigned meta = __float_as_uint(g0.w);
     const float sx = __uint_as_float((meta & 255u) << 23);
@@ -1548,7 +1551,7 @@ __device__ __forceinline__ int wide_node(float4 g0, float4 g1, float4 g2, float4
         const f2 tz = (__builtin_elementwise_fma(qq(qlz, qhz), szz, pz) + noz) * izz;
         const float tn = fmaxf(fmaxf(fminf(tx.x, tx.y), fminf(ty.x, ty.y)), fminf(tz.x, tz.y));
         const float tm = fminf(fminf(fmaxf(tx.x, tx.y), fmaxf(ty.x, ty.y)), fmaxf(tz.x, tz.y));
-        t[i] = (r[i] != INT_MIN && box_hit(tn, tm, cull)) ? tn : INFINITY;   // misses sort last
+        t[i] = (on && r[i] != INT_MIN && box_hit(tn, tm, cull)) ? tn : INFINITY;   // misses sort last
     }
 #else
 #pragma unroll
@@ -1559,10 +1562,10 @@ __device__ __forceinline__ int wide_node(float4 g0, float4 g1, float4 g2, float4
         float tn, tx;
         slab(dq(g0.x, qlx, sx), dq(g0.x, qhx, sx), dq(g0.y, qly, sy), dq(g0.y, qhy, sy), dq(g0.z, qlz, sz),
              dq(g0.z, qhz, sz), R.o, R.ix, R.iy, R.iz, tn, tx);
-        t[i] = (r[i] != INT_MIN && box_hit(tn, tx, cull)) ? tn : INFINITY;   // misses sort last
+        t[i] = (on && r[i] != INT_MIN && box_hit(tn, tx, cull)) ? tn : INFINITY;   // misses sort last
     }
 #endif
-    if (COUNT) {
+    if (COUNT && on) {
         c.nodes++;
         c.boxes += (r[0] != INT_MIN) + (r[1] != INT_MIN) + (r[2] != INT_MIN) + (r[3] != INT_MIN);
     }
@@ -1587,13 +1590,24 @@ __device__ __forceinline__ int wide_node(float4 g0, float4 g1, float4 g2, float4
 // The wide leaf on its loaded record: the exact leaf box, then Moller-Trumbore.  Returns true when
 // an any-hit ray is finished.
 template <bool COUNT>
-__device__ __forceinline__ bool wide_leaf(float4 g0, float4 g1, float4 g2, float4 g3, FastRay& R, Cnt& c) {
-    if (COUNT) { c.tris++; c.boxes++; }
+__device__ __forceinline__ bool wide_leaf(float4 g0, float4 g1, float4 g2, float4 g3, FastRay& R, Cnt& c,
+                                          bool on = true) {   // on = false: no triangle is accepted
+    if (COUNT && on) { c.tris++; c.boxes++; }
     float tn, tx;
     slab(g0.x, g0.w, g0.y, g1.x, g0.z, g1.y, R.o, R.ix, R.iy, R.iz, tn, tx);
     float k;
     const int rank = (int)((~(unsigned)R.item) >> 6);
-    if (box_hit(tn, tx, R.bk * CULL_MARGIN) &&
+#if RT_FLAT_STEP
+    const bool bh = box_hit(tn, tx, R.bk * CULL_MARGIN);
+    const bool mt =
+        mt_core(rtm_v3(g1.z, g1.w, g2.x), rtm_v3(g2.y, g2.z, g2.w), rtm_v3(g3.x, g3.y, g3.z), R.o, R.d, &k);
+    const bool take = on & bh & mt & (k > 0.0001f) & ((k < R.bk) | ((k == R.bk) & (rank < R.brank)));
+    R.bk = take ? k : R.bk;
+    R.bt = take ? 48 * __float_as_int(g3.w) : R.bt;   // the triangle's reference index
+    R.brank = take ? rank : R.brank;
+    return take && R.any;
+#else
+    if (on && box_hit(tn, tx, R.bk * CULL_MARGIN) &&
         mt_core(rtm_v3(g1.z, g1.w, g2.x), rtm_v3(g2.y, g2.z, g2.w), rtm_v3(g3.x, g3.y, g3.z), R.o, R.d, &k) &&
         k > 0.0001f && (k < R.bk || (k == R.bk && rank < R.brank))) {
         R.bk = k;
@@ -1602,6 +1616,7 @@ __device__ __forceinline__ bool wide_leaf(float4 g0, float4 g1, float4 g2, float
         return R.any;
     }
     return false;
+#endif
 }
 
 // One item of the walk over the 4-wide quantised layout (DevScene::wnodes, rt_api.hip emit_wide):
@@ -1620,12 +1635,22 @@ __device__ __forceinline__ bool wide_step(FastRay& R, const char* nb, const char
     const float4 g2 = *reinterpret_cast<const float4*>(p + 32);
     const float4 g3 = *reinterpret_cast<const float4*>(p + 48);
     if (COUNT) count_wave(c.wave_trav);
+#if RT_FLAT_WIDE
+    // both codes on every lane (a step almost always holds node and leaf lanes), predicated
+    const int nx = wide_node<COUNT, OVF>(g0, g1, g2, g3, R, st, c, node);
+    if (wide_leaf<COUNT>(g0, g1, g2, g3, R, c, !node)) return true;
+    if (nx != INT_MIN) {
+        R.item = nx;
+        return false;
+    }
+#else
     if (node) {
         R.item = wide_node<COUNT, OVF>(g0, g1, g2, g3, R, st, c);
         if (R.item != INT_MIN) return false;
     } else if (wide_leaf<COUNT>(g0, g1, g2, g3, R, c)) {
         return true;
     }
+#endif
     while (R.soff > 0) {   // pop the next item still in front of the best hit
         R.soff -= st.stride;
         const int2 en = st.template get<OVF>(R.soff);
