@@ -46,6 +46,8 @@ def main(prof, tag, workload, frames=None, kernel=KERNEL):
     kernel_avg_ms are then per frame (totals / frames).  Default: one dispatch per frame."""
     os.makedirs(os.path.join(ROOT, "profiles"), exist_ok=True)
     stats = glob.glob(os.path.join(prof, "kt", "*kernel_stats.csv"))
+    if not stats:   # a run that never produced its kernel trace must not overwrite committed summaries
+        sys.exit(f"no kernel trace under {prof}/kt")
     s = {"workload": workload, "kernel": kernel, "source": "rocprofv3 (tools/run_profiles.sh)"}
     if stats:
         # every instantiation of the render kernel counts (two-pass launches: pass 1 and pass 2; a
