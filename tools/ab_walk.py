@@ -12,7 +12,7 @@ if len(sys.argv) > 2 and sys.argv[1] == "--one":
         sc, cam, env, npix, spp, mb, ibl = W.CONFIGS[cfg].inputs()
         ctx = _native.Context(device_ids=[0])
         if block: ctx.set_option("block", block)
-        for kv in filter(None, os.environ.get("AB_OPTS_" + name, "").split(";")):   # per-variant options
+        for kv in filter(None, name.partition("@")[2].split("+")):   # NAME@key=value+key=value: options
             k, v = kv.split("=")
             ctx.set_option(k, int(v))
         ctx.set_scene(sc.V_p, sc.V_n, sc.V_uv, sc.faceData, sc.materialData, sc.BVH.exportArray)
@@ -39,7 +39,7 @@ else:
     for spec in sys.argv[1].split(","):
         name, block = spec.split(":")
         env = dict(os.environ)
-        lib = name.split("@")[0]   # NAME@tag: the same library with the options AB_OPTS_NAME@tag
+        lib = name.split("@")[0]   # NAME@key=value+...: the library NAME with these rt_set_option values
         if lib != "base":
             env["ENSEM3A_RT_LIB"] = os.path.join(VDIR, f"lib{lib}.so")
         r = subprocess.run([sys.executable, __file__, "--one", name, block, os.environ.get("AB_CFGS", "C3,C4")],
