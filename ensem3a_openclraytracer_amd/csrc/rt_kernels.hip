@@ -1284,6 +1284,9 @@ constexpr unsigned kLeafTail = 40u;
 #ifndef RT_FLAT_STEP
 #define RT_FLAT_STEP 1
 #endif
+#ifndef RT_FLAT_TEAM
+#define RT_FLAT_TEAM RT_FLAT_STEP
+#endif
 __device__ __forceinline__ float4 leaf_e2(float4 g2, int2 tail) {
     return make_float4(g2.x, g2.y, __int_as_float(tail.x), g2.w);
 }
@@ -1443,7 +1446,7 @@ __device__ __forceinline__ bool team_step(int ts, FastRay& R, unsigned& boff, co
         const float4 g1 = *reinterpret_cast<const float4*>(p + ks);
         const float4 g2 = *reinterpret_cast<const float4*>(p + 2 * ks);
         const int2 e = *reinterpret_cast<const int2*>(p + (node ? 3 * ks : kLeafTail));
-#if RT_FLAT_STEP
+#if RT_FLAT_TEAM
         // both tests, outcomes by selects (fast_step)
         const float cull = R.bk * CULL_MARGIN;
         float t0n, t0x, t1n, t1x;
