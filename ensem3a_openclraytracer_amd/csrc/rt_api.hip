@@ -50,6 +50,7 @@ struct Device {
     DevBuf stack_ovf;             // FAST traversal stack entries beyond the LDS part
     DevBuf nodes, wnodes, wleaves, tri_fast, brute, brute_box, bvh9, tri_geo, tri_shade, tri_frame, mat, ibl, out, out8, counts, work, scratch_a, scratch_b;
     DevBuf pilot;                 // two-pass launches: per-pixel state, cost and order (FrameParams::pilot_*)
+    DevBuf wf;                    // wavefront launches: the waves' path-state regions (FrameParams::wf_buf)
     char* host_stage = nullptr;   // pinned staging for rt_render / rt_render_rgb8
     size_t host_stage_bytes = 0;
     // Every launch of this context on the device shares `work` (pixel counters + launch constants)
@@ -109,6 +110,7 @@ struct rt_ctx {
     int pilot_chunk = 0;  // pixels ordered together (0 = auto: 64 brute force, 1 tree walk)
     int pilot_levels = 0; // cost bins of the order (0 = auto: 256)
     int stack_lds = 0;    // FAST stack entries per lane kept in LDS (0 = auto: rt::kStackLds, kStackLdsWide)
+    int wavefront = -1;   // tree walk split into trace / shade phases: path slots per lane (0 = off, -1 = auto)
     std::string err;
 };
 
@@ -654,6 +656,13 @@ rt::DevScene dev_scene(const rt_ctx* ctx, const Device& d) {
     return s;
 }
 
+// option "wavefront" -1 (auto): path slots per lane of the wavefront walk, 0 = the per-lane megakernel
+int auto_wavefront(const rt_ctx* ctx, const rt::FrameParams& fp) {
+    (void)ctx;
+    (void)fp;
+    return 0;
+}
+
 int check_frame(rt_ctx* ctx, const float* cam, const float* env, int64_t npix, int spp, int row0, int row_step,
                 rt::FrameParams* fp) {
     if (!ctx) return set_err(nullptr, RT_ERR_ARG, "null context");
@@ -692,6 +701,8 @@ int check_frame(rt_ctx* ctx, const float* cam, const float* env, int64_t npix, i
     fp->team = ctx->team;
     fp->walk_team = ctx->walk_team;
     fp->max_waves = ctx->max_waves;
+    fp->wf_slots = ctx->wavefront > 0 ? ctx->wavefront : (ctx->wavefront < 0 ? auto_wavefront(ctx, *fp) : 0);
+    fp->wf_buf = nullptr;
     fp->log_buf = nullptr;
     fp->log_cap = 0;
     fp->log_count = nullptr;
@@ -750,7 +761,7 @@ void rt_destroy(rt_ctx* ctx) {
         if (d.pending) (void)hipEventSynchronize(d.done);
         if (d.stream) (void)hipStreamSynchronize(d.stream);
         for (DevBuf* b : {&d.stack_ovf, &d.nodes, &d.wnodes, &d.wleaves, &d.tri_fast, &d.brute, &d.brute_box, &d.bvh9, &d.tri_geo, &d.tri_shade, &d.tri_frame, &d.mat, &d.ibl, &d.out,
-                          &d.out8, &d.counts, &d.work, &d.scratch_a, &d.scratch_b, &d.pilot})
+                          &d.out8, &d.counts, &d.work, &d.scratch_a, &d.scratch_b, &d.pilot, &d.wf})
             release(*b);
         if (d.host_stage) (void)hipHostFree(d.host_stage);
         if (d.stream) (void)hipStreamDestroy(d.stream);
@@ -871,6 +882,11 @@ int rt_set_option(rt_ctx* ctx, const char* key, int64_t value) {
     if (!std::strcmp(key, "bvh_width")) {
         if (value != 0 && value != 2 && value != 4) return set_err(ctx, RT_ERR_ARG, "bvh_width must be 0 (auto), 2 or 4");
         ctx->bvh_width = (int)value;
+        return RT_OK;
+    }
+    if (!std::strcmp(key, "wavefront")) {
+        if (value < -1 || value > 16) return set_err(ctx, RT_ERR_ARG, "wavefront must be -1 (auto), 0 (off) or 1..16");
+        ctx->wavefront = (int)value;
         return RT_OK;
     }
     if (!std::strcmp(key, "block")) {
@@ -1028,7 +1044,7 @@ namespace {
 // or K), whose per-pixel costs order the rest of the frame, most expensive first (rt_kernels.hip
 // launch_render).  Sets fp's pilot fields and sizes the device's scratch for them.
 hipError_t setup_pilot(rt_ctx* ctx, Device& d, rt::FrameParams& fp) {
-    if (ctx->pilot == 0 || effective_traversal(ctx) != RT_TRAVERSAL_FAST || fp.nloc <= 0) return hipSuccess;
+    if (fp.wf_buf || ctx->pilot == 0 || effective_traversal(ctx) != RT_TRAVERSAL_FAST || fp.nloc <= 0) return hipSuccess;
     int k = ctx->pilot;
     if (k < 0) {   // auto: the tree walk on tiles of 1-16 pixels per resident lane (where the tail is long)
         const int64_t lanes = (int64_t)std::max(d.cus, 1) * 1280;
@@ -1068,6 +1084,31 @@ hipError_t setup_pilot(rt_ctx* ctx, Device& d, rt::FrameParams& fp) {
 }
 }  // namespace
 
+namespace {
+// Wavefront launches (FrameParams::wf_slots): size the device's path-state regions, or fall back to
+// the megakernel (wf_slots = 0) where the launch cannot take the wavefront walk
+hipError_t setup_wavefront(rt_ctx* ctx, Device& d, rt::FrameParams& fp) {
+    fp.wf_buf = nullptr;
+    if (fp.wf_slots <= 0 || effective_traversal(ctx) != RT_TRAVERSAL_FAST) {
+        fp.wf_slots = 0;
+        return hipSuccess;
+    }
+    const rt::DevScene ds = dev_scene(ctx, d);
+    if (!rt::wavefront_eligible(ds, fp)) {
+        fp.wf_slots = 0;
+        return hipSuccess;
+    }
+    const size_t need = rt::wavefront_bytes(ds, fp, ctx->block);
+    hipError_t e = hipSuccess;
+    // growing frees the old buffer from the host: the last launch (any stream) may still use it
+    if (d.wf.bytes < need && d.pending) e = hipEventSynchronize(d.done);
+    if (e == hipSuccess) e = ensure(d.wf, need);
+    if (e != hipSuccess) return e;
+    fp.wf_buf = (float*)d.wf.p;
+    return hipSuccess;
+}
+}  // namespace
+
 int rt_render_device(rt_ctx* ctx, int device_index, const float cam[10], const float env[5], int64_t npix, int spp,
                      int max_bounce, int row0, int row_step, float* d_out, void* stream) {
     rt::FrameParams fp;
@@ -1082,6 +1123,7 @@ int rt_render_device(rt_ctx* ctx, int device_index, const float cam[10], const f
     HIP_OR_RET(ctx, hipSetDevice(d.id));
     hipStream_t s = (hipStream_t)stream;  // NULL = the device's default (null) stream, HIP convention
     HIP_OR_RET(ctx, order_after_last(d, s));
+    HIP_OR_RET(ctx, setup_wavefront(ctx, d, fp));
     HIP_OR_RET(ctx, setup_pilot(ctx, d, fp));
     HIP_OR_RET(ctx, rt::launch_render(dev_scene(ctx, d), fp, effective_traversal(ctx), ctx->block, d_out, nullptr,
                                       (unsigned int*)d.work.p, s));
@@ -1142,6 +1184,7 @@ int render_host(rt_ctx* ctx, const float cam[10], const float env[5], int64_t np
             d.host_stage_bytes = bytes;
         }
         HIP_OR_RET(ctx, order_after_last(d, d.stream));
+        HIP_OR_RET(ctx, setup_wavefront(ctx, d, fp));
         HIP_OR_RET(ctx, setup_pilot(ctx, d, fp));
         HIP_OR_RET(ctx, rt::launch_render(dev_scene(ctx, d), fp, effective_traversal(ctx), ctx->block,
                                           (float*)d.out.p, nullptr, (unsigned int*)d.work.p, d.stream));
@@ -1234,6 +1277,7 @@ int count_all(rt_ctx* ctx, const float cam[10], const float env[5], int64_t npix
     HIP_OR_RET(ctx, ensure(d.counts, sizeof h));
     HIP_OR_RET(ctx, hipMemsetAsync(d.counts.p, 0, sizeof h, d.stream));
     HIP_OR_RET(ctx, order_after_last(d, d.stream));
+    HIP_OR_RET(ctx, setup_wavefront(ctx, d, fp));
     HIP_OR_RET(ctx, rt::launch_render(dev_scene(ctx, d), fp, effective_traversal(ctx), ctx->block, (float*)d.out.p,
                                       (unsigned long long*)d.counts.p, (unsigned int*)d.work.p, d.stream));
     HIP_OR_RET(ctx, mark_launch(d, d.stream));

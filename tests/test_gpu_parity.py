@@ -989,3 +989,39 @@ def test_two_pass_pilot_full_frame(kl, config, pilot, spp):
     finally:
         ctx.close()
     np.testing.assert_array_equal(out[pilot], out[0])
+
+
+@pytest.mark.parametrize("case", ["monkey_c3_64_s4", "serre_96x54_s4", "proto_64_s4", "furnace_64_s4", "grid"])
+def test_wavefront_renders_identically(kl, case):
+    """wavefront K: each persistent wave keeps 64 K paths in HBM and alternates a shade phase (naiveGI's
+    logic for every path, new pixels, the live paths compacted into the wave's ray queue) with a trace
+    phase (lanes take queued rays as soon as theirs is done).  One ray in flight per pixel and the
+    megakernel's shading order: the frame and every work counter are the megakernel's, bit for bit,
+    on both tree layouts (BVH2 with the glass prefix; 4-wide, the grid case spilling its stack to HBM)."""
+    if case == "grid":
+        sc, cam, env, npix, spp, mb, ibl = W.CONFIGS["C5"].with_size(48, 27, 2).inputs()
+    else:
+        sc, cam, env, npix, spp, mb, ibl = W.PARITY_CASES[case].inputs()
+    want = _oracle(sc, cam, env, npix, spp, mb, ibl)
+    kl.native.set_option("brute_max", 0)   # the tree walk, also for small scenes
+    try:
+        for width in (2, 4):
+            kl.native.set_option("bvh_width", width)
+            kl.native.set_option("wavefront", 0)
+            base = _launch(kl, sc, cam, env, npix, spp, mb, ibl, "fast")
+            c0 = kl.native.count_work_detail(cam, env, npix, spp, mb)
+            for k in (1, 2, 3, 4, 8):
+                kl.native.set_option("wavefront", k)
+                got = _launch(kl, sc, cam, env, npix, spp, mb, ibl, "fast")
+                np.testing.assert_array_equal(got, base, err_msg=f"width {width} K {k}")
+                ck = kl.native.count_work_detail(cam, env, npix, spp, mb)
+                for key in ("rays", "samples", "ev_diffuse", "ev_glossy", "ev_glass", "sun_terms", "env_lookups",
+                            "node_fetches", "tri_tests", "box_tests"):
+                    assert ck[key] == c0[key], (width, k, key, ck[key], c0[key])
+            np.testing.assert_array_equal(base, want)
+    finally:
+        kl.native.set_option("wavefront", -1)
+        kl.native.set_option("bvh_width", 0)
+        kl.native.set_option("brute_max", 64)
+    with pytest.raises(_native.NativeError, match="wavefront"):
+        kl.native.set_option("wavefront", 17)

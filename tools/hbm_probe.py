@@ -1,7 +1,7 @@
-"""Summarise tools/hbm_probe.sh passes over tools/hbm_probe (the counter calibration) into
-profiles/r03_hbm_probe.json.
+"""Calibration of the L2 memory-side byte counters on reads of known size (tools/hbm_probe.hip).
 
-    python tools/hbm_probe_summary.py gpurun_out/hbm_probe [OUT_JSON]
+    python tools/hbm_probe.py run OUTDIR -- PROGRAM [ARGS...]   (GPU box: one rocprofv3 pass per counter group)
+    python tools/hbm_probe.py summary OUTDIR [OUT_JSON]         (-> profiles/r03_hbm_probe.json)
 
 For every probe kernel (its second dispatch: the first warms the TLB): the known bytes it reads, each
 counter, and the byte figures they imply --
@@ -17,9 +17,34 @@ import re
 import glob
 import json
 import os
+import subprocess
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+# one counter group per rocprofv3 run (at most 4 TCC counters a pass)
+PASSES = {
+    "kt": ["--kernel-trace", "--stats"],
+    "fetch": ["--pmc", "FETCH_SIZE"],
+    "write": ["--pmc", "WRITE_SIZE"],
+    "req": ["--pmc", "TCC_EA0_RDREQ_sum", "TCC_EA0_RDREQ_32B_sum", "TCC_EA0_RDREQ_64B_sum", "TCC_EA0_RDREQ_128B_sum"],
+    "dram": ["--pmc", "TCC_BUBBLE_sum", "TCC_EA0_RDREQ_DRAM_sum", "TCC_EA0_RDREQ_DRAM_32B_sum", "TCC_MISS_sum"],
+    "hit": ["--pmc", "TCC_HIT_sum", "TCC_REQ_sum", "TCC_READ_sum", "TCC_EA0_WRREQ_64B_sum"],
+}
+
+
+def run(out, prog):
+    """Every pass of PASSES over the program, each under its own time limit; stops at a failure."""
+    os.makedirs(out, exist_ok=True)
+    env = dict(os.environ, TMPDIR="/tmp")
+    for name, args in PASSES.items():
+        print("pass", name, flush=True)
+        with open(os.path.join(out, name + ".log"), "w") as log:
+            subprocess.run(["timeout", "-s", "KILL", os.environ.get("PASS_TIMEOUT", "120"), "rocprofv3"] + args +
+                           ["--output-format", "csv", "-d", os.path.join(out, name), "-o", name, "--"] + prog,
+                           stdout=log, stderr=subprocess.STDOUT, env=env, check=True)
+    print("passes done:", out)
+
+
 def _rows(pattern):
     out = []
     for p in glob.glob(pattern):
@@ -39,7 +64,7 @@ def kernel_key(name: str) -> str:
     return "gather64_mall" if re.search(r"false, 0>", name) else "gather64_dram"
 
 
-def main(prof, out=None):
+def summary(prof, out=None):
     known = {}
     for line in open(os.path.join(prof, "kt.log")):
         line = line.strip()
@@ -66,7 +91,7 @@ def main(prof, out=None):
             seen.setdefault((kernel_key(n), c), []).append(v)
         for (key, c), vs in seen.items():
             table.setdefault(key, {})[c] = vs[-1]   # the second dispatch
-    summary = {"source": "tools/hbm_probe.hip under tools/hbm_probe.sh (rocprofv3, one counter group per pass)",
+    summary = {"source": "tools/hbm_probe.hip under tools/hbm_probe.py run (rocprofv3, one counter group per pass)",
                "kernels": {}}
     for key, d in known.items():
         t = table.get(key, {})
@@ -93,4 +118,8 @@ def main(prof, out=None):
 
 
 if __name__ == "__main__":
-    main(*sys.argv[1:3])
+    if sys.argv[1] == "run":
+        a = sys.argv[3:]
+        run(sys.argv[2], a[1:] if a and a[0] == "--" else a)
+    else:
+        summary(*sys.argv[2:4])
