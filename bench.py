@@ -30,8 +30,8 @@ Extra fields (DESIGN.md 5 derives every number):
                    (SQ_INSTS_VALU x 64) per launch, when committed.
   host_boundary -- rt_render (launch_Raytracing's blocking C-ABI: kernel + copy of
                    the frame into caller memory), timed over the same W/K steps.
-  configs       -- C3 and C4 timed the same way (2 steps, 1 warmup), C5 (1 step, 1 warmup: 5-6 s
-                   per frame); at N=1 on one device (with their roofline), at N>1 through the same
+  configs       -- C3, C4 and C5 timed the same way (2 steps, 1 warmup; per-frame min / median and the
+                   GPU clock beside them); at N=1 on one device (with their roofline), at N>1 through the same
                    row tiles + RCCL gather as the headline (every config's strong scaling).
   cpu_baseline  -- the CPU oracle (a C restatement of the reference kernel, OpenMP)
                    timed on this host on a bounded row sample of the same frame.
@@ -215,8 +215,62 @@ def cpu_baseline(wl, scene, ibl, cam, env, target_s: float = 10.0):
                            "itself 2.06-2.14 (BASELINE.md 2): 0.89-0.92x (DESIGN.md 5)"}
 
 
+def gpu_clock() -> dict:
+    """The GPU's current / allowed shader clocks from amd-smi (rocm-smi as a fallback), logged beside the
+    long timings so that box-to-box clock differences are visible; {} when no tool answers."""
+    import re
+    import subprocess
+    for cmd in (["amd-smi", "metric", "-c"], ["rocm-smi", "--showclocks"]):
+        try:
+            txt = subprocess.run(cmd, capture_output=True, text=True, timeout=20).stdout
+        except (OSError, subprocess.SubprocessError):
+            continue
+        m = re.search(r"GFX_0:\s*CLK:\s*(\d+)\s*MHz\s*MIN_CLK:\s*(\d+)\s*MHz\s*MAX_CLK:\s*(\d+)", txt, re.S)
+        if m:
+            return {"tool": cmd[0], "sclk_mhz": int(m.group(1)), "min_mhz": int(m.group(2)), "max_mhz": int(m.group(3))}
+        m = re.search(r"sclk.*?(\d+)\s*Mhz", txt, re.I)
+        if m:
+            return {"tool": cmd[0], "sclk_mhz": int(m.group(1))}
+    return {}
+
+
+class ClockSampler:
+    """Polls gpu_clock() on a host thread while a timed region runs (amd-smi is a separate process: the
+    GPU's idle clock after a run says nothing, its clock during the frames does)."""
+
+    def __init__(self):
+        import threading
+        self.samples, self.max_mhz, self._stop = [], None, threading.Event()
+        self._t = threading.Thread(target=self._run, daemon=True)
+
+    def _run(self):
+        while not self._stop.is_set():
+            c = gpu_clock()
+            if not c:
+                return
+            self.samples.append(c["sclk_mhz"])
+            self.max_mhz = c.get("max_mhz")
+            self._stop.wait(0.5)
+
+    def __enter__(self):
+        self._t.start()
+        return self
+
+    def __exit__(self, *a):
+        self._stop.set()
+        self._t.join(timeout=30)
+
+    def summary(self) -> dict:
+        if not self.samples:
+            return {}
+        return {"tool": "amd-smi metric -c (GFX_0), polled during the timed frames", "samples": len(self.samples),
+                "sclk_mhz_min": min(self.samples), "sclk_mhz_median": float(np.median(self.samples)),
+                "sclk_mhz_max": max(self.samples), "max_mhz": self.max_mhz}
+
+
 def time_config(ctx_factory, name: str, steps: int, warmup: int):
-    """One-GPU device-resident timing of another BASELINE config (C3/C4/C5), same method as the headline."""
+    """One-GPU device-resident timing of another BASELINE config (C3/C4/C5), same method as the headline;
+    every frame is timed on its own (HIP events) and min / median reported beside the mean."""
     import torch
     from ensem3a_openclraytracer_amd import workloads as Wk
     wl = Wk.CONFIGS[name]
@@ -230,19 +284,24 @@ def time_config(ctx_factory, name: str, steps: int, warmup: int):
     for _ in range(warmup):
         ctx.render_device(cam, env, npix, spp, mb, 0, 1, out.data_ptr(), stream.cuda_stream)
     torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for i in range(steps):
-        ev[i][0].record(stream)
-        ctx.render_device(cam, env, npix, spp, mb, 0, 1, out.data_ptr(), stream.cuda_stream)
-        ev[i][1].record(stream)
-    torch.cuda.synchronize()
-    dt = (time.perf_counter() - t0) / steps
-    kernel_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    with ClockSampler() as clk:
+        t0 = time.perf_counter()
+        for i in range(steps):
+            ev[i][0].record(stream)
+            ctx.render_device(cam, env, npix, spp, mb, 0, 1, out.data_ptr(), stream.cuda_stream)
+            ev[i][1].record(stream)
+        torch.cuda.synchronize()
+        dt = (time.perf_counter() - t0) / steps
+    per = [a.elapsed_time(b) for a, b in ev]
+    kernel_ms = float(np.mean(per))
     cnt = ctx.count_work_detail(cam, env, npix, spp, mb)
     rf = roofline(ctx, cnt, kernel_ms, npix, wl.name)
     ctx.close()
     return {"workload": wl.name, "value": round(npix * spp / dt / 1e6, 3), "unit": "Msamples/s",
             "ms_per_step": round(dt * 1e3, 3), "steps": steps, "warmup": warmup,
+            "frame_ms": {"min": round(min(per), 3), "median": round(float(np.median(per)), 3),
+                         "max": round(max(per), 3)},
+            "gpu_clock": clk.summary(),
             "roofline": {k: rf.get(k) for k in ("bound", "achieved", "peak", "unit", "frac", "traffic", "traffic_frac",
                                                 "hbm_measured", "kernel_ms", "path", "profile")},
             "valu_frac": rf["frac"] if rf["bound"] == "valu" else rf["other_bound"]["frac"]}
@@ -480,7 +539,7 @@ def main():
             ctx.close()
             ctx = None
             line["configs"] = {c: time_config(make_ctx, c, 2, 1) for c in ("C3", "C4")}
-            line["configs"]["C5"] = time_config(make_ctx, "C5", 1, 1)
+            line["configs"]["C5"] = time_config(make_ctx, "C5", 2, 1)
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(wl, scene, ibl, cam, env)
         print(json.dumps(line), flush=True)

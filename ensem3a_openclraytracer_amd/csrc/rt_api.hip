@@ -111,6 +111,7 @@ struct rt_ctx {
     int pilot_levels = 0; // cost bins of the order (0 = auto: 256)
     int stack_lds = 0;    // FAST stack entries per lane kept in LDS (0 = auto: rt::kStackLds, kStackLdsWide)
     int wavefront = -1;   // tree walk split into trace / shade phases: path slots per lane (0 = off, -1 = auto)
+    int ref_stack = 20;   // REF traversal stack capacity (20 = the reference's, stack.cl:4)
     std::string err;
 };
 
@@ -633,6 +634,7 @@ rt::DevScene dev_scene(const rt_ctx* ctx, const Device& d) {
     for (int k = 0; k < 6; ++k) s.root_box[k] = ctx->hs.root_box[k];
     s.bvh9 = (const float*)d.bvh9.p;
     s.nbvh9 = ctx->hs.nbvh9;
+    s.ref_stack = ctx->ref_stack;
     s.tri_geo = (const float4*)d.tri_geo.p;
     s.tri_fast = (const float4*)d.tri_fast.p;
     s.tri_shade = (const float4*)d.tri_shade.p;
@@ -882,6 +884,11 @@ int rt_set_option(rt_ctx* ctx, const char* key, int64_t value) {
     if (!std::strcmp(key, "bvh_width")) {
         if (value != 0 && value != 2 && value != 4) return set_err(ctx, RT_ERR_ARG, "bvh_width must be 0 (auto), 2 or 4");
         ctx->bvh_width = (int)value;
+        return RT_OK;
+    }
+    if (!std::strcmp(key, "ref_stack")) {
+        if (value < 20 || value > 64) return set_err(ctx, RT_ERR_ARG, "ref_stack must be in 20..64 (20 = the reference's)");
+        ctx->ref_stack = (int)value;
         return RT_OK;
     }
     if (!std::strcmp(key, "wavefront")) {
@@ -1145,8 +1152,15 @@ void par_copy(char* dst, const char* src, size_t n) {
     }
     const size_t chunk = ((n + k - 1) / k + 4095) & ~(size_t)4095;
     std::vector<std::thread> ts;
-    for (size_t i = 1; i < k && i * chunk < n; ++i)
-        ts.emplace_back([=] { std::memcpy(dst + i * chunk, src + i * chunk, std::min(chunk, n - i * chunk)); });
+    size_t i = 1;
+    // a thread that cannot be created (a thread / cgroup limit) must not throw across the C ABI: the
+    // chunks no thread took are copied here
+    try {
+        for (; i < k && i * chunk < n; ++i)
+            ts.emplace_back([=] { std::memcpy(dst + i * chunk, src + i * chunk, std::min(chunk, n - i * chunk)); });
+    } catch (...) {
+    }
+    for (size_t r = i; r < k && r * chunk < n; ++r) std::memcpy(dst + r * chunk, src + r * chunk, std::min(chunk, n - r * chunk));
     std::memcpy(dst, src, std::min(chunk, n));
     for (auto& t : ts) t.join();
 }

@@ -20,7 +20,7 @@ constexpr size_t kLdsSceneMax = 24 * 1024;
 
 constexpr int TRAV_FAST = 0;
 constexpr int TRAV_REF = 1;
-constexpr int REF_STACK = 20;  // stack.cl:4, Raytracing capacity 20
+constexpr int REF_STACK = 20;  // stack.cl:4, Raytracing capacity 20 (DevScene::ref_stack: the REF traversal's cap)
 
 struct Hit {
     float k;
@@ -116,12 +116,12 @@ __device__ Hit trace_ref(const DevScene& S, rtm_f3 o, rtm_f3 d, int* __restrict_
             }
             const int L = (int)nd[0];
             if (L != -1) {
-                if (top == REF_STACK - 1) { if (COUNT) c.dropped++; }
+                if (top == S.ref_stack - 1) { if (COUNT) c.dropped++; }
                 else stk[(++top) * B] = L;
             }
             const int R = (int)nd[1];
             if (R != -1) {
-                if (top == REF_STACK - 1) { if (COUNT) c.dropped++; }
+                if (top == S.ref_stack - 1) { if (COUNT) c.dropped++; }
                 else stk[(++top) * B] = R;
             }
         }
@@ -220,10 +220,13 @@ struct LaneStack {
         else e = ovf[slot(off)];
         return e;
     }
-    // entry `off` of the stack of the lane dl lanes away in the same wave (team walk steals)
+    // entry `off` of the stack of the lane dl lanes away in the same wave (team walk steals).  The
+    // teammate wrote it in an earlier step of this wave; the wavefront-scope acquire fence orders the read
+    // after those writes (LDS and the HBM overflow part alike)
     template <bool OVF>
     __device__ __forceinline__ int2 get_lane(unsigned off, int dl) const {
         int2 e;
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         if (!OVF || off < cap) e = unpack_entry(*(const lds_u64*)(lds + off + 8 * dl));
         else e = ovf[(unsigned)((int)slot(off) + dl)];
         return e;
@@ -554,7 +557,9 @@ struct LaunchConst {
     float pas;                        // 1.0 / cam[6]
 };
 
-__device__ __forceinline__ LaunchConst make_const(const FrameParams& F) {  // evaluated once per launch
+// evaluated once per launch: on the device (make_const_kernel) or on the host (the wavefront launch passes
+// it by value); rtm.h makes both bit-identical
+__host__ __device__ inline LaunchConst make_const(const FrameParams& F) {
     LaunchConst c;
     const float* cam = F.cam;
     c.focal = rtm_v3(cam[0], cam[1] - (1.0f / (2.0f * rtm_tan(cam[9] / 2.0f))), cam[2]);

@@ -56,6 +56,10 @@ struct DevScene {
     // REF traversal: the reference's own AoS export, 9 floats per node
     const float* bvh9;
     int32_t nbvh9;
+    // REF traversal stack capacity: 20 = the reference's (stack.cl:4; a push onto a full stack is dropped,
+    // stack.cl:23-24); up to 64 (option "ref_stack") renders the reference's DFS without drops, which
+    // separates the pixels a drop changes from those the FAST slab rounding changes
+    int32_t ref_stack;
     // triangles in reference order: 3 x float4 (a.p | rank, e1 | index, e2 | 0); REF traversal
     const float4* tri_geo;
     // the same records in the order the FAST tree's leaves are met depth-first (the FAST leaf refs

@@ -787,7 +787,7 @@ template <int TRAV, bool COUNT, bool LOG, bool SMEM = false, bool RESUME = false
 hipError_t launch_t(const DevScene& sc, const FrameParams& fp, int block, float* d_out, unsigned long long* d_counts,
                     unsigned int* d_work, hipStream_t stream) {
     // FAST: int2 entries; the brute-force path of small scenes needs no stack
-    const int depth = (TRAV == TRAV_REF) ? REF_STACK : (sc.nbrute > 0 ? 1 : 2 * (sc.stack_lds > 0 ? sc.stack_lds : 1));
+    const int depth = (TRAV == TRAV_REF) ? sc.ref_stack : (sc.nbrute > 0 ? 1 : 2 * (sc.stack_lds > 0 ? sc.stack_lds : 1));
     size_t lds = (size_t)depth * block * sizeof(int);
     if (TRAV == TRAV_FAST && sc.nbrute > 0) lds = std::max(lds, (size_t)(block / 64) * BRUTE_WAVE_LDS);
     if (BRUTE)
@@ -973,7 +973,7 @@ hipError_t launch_debug_trace(const DevScene& sc, int traversal, const float* ra
     DevScene s2 = sc;
     s2.stack_lds = sc.depth > 0 ? sc.depth : 1;
     s2.stack_ovf = nullptr;
-    const int depth = traversal == TRAV_REF ? REF_STACK : 2 * s2.stack_lds;
+    const int depth = traversal == TRAV_REF ? s2.ref_stack : 2 * s2.stack_lds;
     size_t lds = (size_t)depth * block * sizeof(int);
     if (traversal != TRAV_REF && sc.nbrute > 0) lds = std::max(lds, (size_t)(block / 64) * BRUTE_WAVE_LDS);
     if (traversal == TRAV_REF)

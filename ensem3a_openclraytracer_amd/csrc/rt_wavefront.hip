@@ -67,18 +67,42 @@ __device__ __forceinline__ float as_f(int i) { return __int_as_float(i); }
 // position pos may overwrite the row another lane of the wave read at q = pos in this sub-round.
 __device__ __forceinline__ void wait_loads() { __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
+// The kernel's parameters (scene, frame, launch constants) as one struct, laid out as the kernel
+// argument segment lays them out (each argument at its natural alignment, in order)
+struct WfArgs {
+    DevScene S;
+    FrameParams F;
+    LaunchConst C;
+};
+
+// RT_WF_OPAQUE: the parameters are re-read (scalar loads from the kernel argument segment, through a
+// pointer the compiler cannot see through) at the start of every shade sub-round and trace phase, so
+// that the values only one phase uses are not held in SGPRs across the other (SGPR spills into VGPR lanes)
+#ifndef RT_WF_OPAQUE
+#define RT_WF_OPAQUE 1
+#endif
+#if RT_WF_OPAQUE
+typedef const char __attribute__((address_space(4))) kernarg_char;
+#define WF_REFRESH_PARAMS                                                                         \
+    kernarg_char* kap_ = (kernarg_char*)__builtin_amdgcn_kernarg_segment_ptr();                     \
+    __asm__ volatile("" : "+s"(kap_));                                                             \
+    const WfArgs& wa_ = *(const WfArgs*)kap_;                                                      \
+    const DevScene& S = wa_.S;                                                                     \
+    const FrameParams& F = wa_.F;                                                                  \
+    const LaunchConst& C = wa_.C;                                                                  \
+    (void)S; (void)F; (void)C;
+#else
+#define WF_REFRESH_PARAMS
+#endif
+
 template <bool COUNT, bool OVF, bool WIDE>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kWfWaves)))
-wave_kernel(DevScene S, FrameParams F, float* __restrict__ out, unsigned long long* __restrict__ counts,
-            unsigned int* __restrict__ work_counter, const LaunchConst* __restrict__ lconst) {
+wave_kernel(DevScene S, FrameParams F, LaunchConst C, float* __restrict__ out, unsigned long long* __restrict__ counts,
+            unsigned int* __restrict__ work_counter) {
     constexpr bool PREFIX = !WIDE;
     constexpr int NPL = wf_planes(PREFIX);
     extern __shared__ int lds_stack[];
     Cnt c{};
-    const LaunchConst& C = *lconst;
-    const LaneStack lst = lane_stack(S, lds_stack);
-    const char* const nb = reinterpret_cast<const char*>(WIDE ? S.wnodes : S.nodes);
-    const char* const tb = reinterpret_cast<const char*>(WIDE ? S.wleaves : S.tri_fast);
     const int lane = threadIdx.x & 63;
     const unsigned SW = 64u * (unsigned)F.wf_slots;   // paths of this wave
     // the wave's index, wave-uniform (readfirstlane: its region's pointers live in SGPRs)
@@ -90,15 +114,6 @@ wave_kernel(DevScene S, FrameParams F, float* __restrict__ out, unsigned long lo
     float2* const hb = reinterpret_cast<float2*>(rb1 + SW);
     auto P = [&](int f, unsigned q) -> float& { return pl[(unsigned)f * SW + q]; };
 
-    const int W = F.width;
-    const int imgSize = (int)F.npix;
-    const float e3 = F.env[3], e4 = F.env[4];
-    const int spp = F.spp, maxB = F.max_bounce;
-    const unsigned nloc = (unsigned)F.nloc;
-    auto global_pixel = [&](int p) -> int64_t {
-        const int krow = p / W;
-        return ((int64_t)F.row0 + (int64_t)krow * F.row_step) * W + (p - krow * W);
-    };
 
     PixelQueue pq;
     unsigned n = SW;     // queue entries (wave-uniform); the first shade phase: every slot takes a pixel
@@ -108,6 +123,16 @@ wave_kernel(DevScene S, FrameParams F, float* __restrict__ out, unsigned long lo
         const unsigned long long t_shade = COUNT ? clock64() : 0;
         unsigned nout = 0;
         for (unsigned r0 = 0; r0 < n; r0 += 64) {
+            WF_REFRESH_PARAMS
+            const int W = F.width;
+            const int imgSize = (int)F.npix;
+            const float e3 = F.env[3], e4 = F.env[4];
+            const int spp = F.spp, maxB = F.max_bounce;
+            const unsigned nloc = (unsigned)F.nloc;
+            auto global_pixel = [&](int p) -> int64_t {
+                const int krow = p / W;
+                return ((int64_t)F.row0 + (int64_t)krow * F.row_step) * W + (p - krow * W);
+            };
             if (COUNT && lane == 0) c.wave_outer++;
             const unsigned q = r0 + (unsigned)lane;
             const bool valid = q < n;
@@ -323,13 +348,7 @@ wave_kernel(DevScene S, FrameParams F, float* __restrict__ out, unsigned long lo
             const unsigned long long m = __ballot(live);
             const unsigned pos = lane_prefix(m, nout);
             const bool moved = pos != q;
-            // a moved path's glass prefix is copied to its new row (loaded before any row is overwritten)
-            float pre_row[12];
             const bool copy_pre = PREFIX && live && moved && pre;
-            if (copy_pre) {
-#pragma unroll
-                for (int f = 0; f < 12; ++f) pre_row[f] = P(WF_PJ + f, q);
-            }
             wait_loads();
             if (live) {
                 const unsigned fl = (unsigned)phase | (drew ? 8u : 0u) | (fdb ? 16u : 0u) | (pre ? 32u : 0u) |
@@ -350,9 +369,14 @@ wave_kernel(DevScene S, FrameParams F, float* __restrict__ out, unsigned long lo
                     P(WF_TC, pos) = as_f(tc);
                 }
                 if (moved || (dirty & D_SUNC)) P(WF_SC, pos) = as_f(sun_c);
-                if (copy_pre) {
-#pragma unroll
-                    for (int f = 0; f < 12; ++f) P(WF_PJ + f, pos) = pre_row[f];
+            }
+            // a moved path's glass prefix goes to its new row plane by plane: every lane's read of a plane
+            // returns before any lane writes that plane (the other planes are not touched in between)
+            if (copy_pre) {
+                for (int f = 0; f < 12; ++f) {
+                    const float v = P(WF_PJ + f, q);
+                    wait_loads();
+                    P(WF_PJ + f, pos) = v;
                 }
             }
             nout += (unsigned)__popcll(m);
@@ -362,6 +386,10 @@ wave_kernel(DevScene S, FrameParams F, float* __restrict__ out, unsigned long lo
         if (n == 0) break;
 
         // ================= trace phase =================
+        WF_REFRESH_PARAMS
+        const LaneStack lst = lane_stack(S, lds_stack);
+        const char* const nb = reinterpret_cast<const char*>(WIDE ? S.wnodes : S.nodes);
+        const char* const tb = reinterpret_cast<const char*>(WIDE ? S.wleaves : S.tri_fast);
         const unsigned long long t_trace = COUNT ? clock64() : 0;
         if (COUNT && lane == 0) c.cyc_shade += t_trace - t_shade;
         FastRay T;
@@ -474,14 +502,12 @@ hipError_t launch_wavefront(const DevScene& sc, const FrameParams& fp, int block
                                            (int64_t)cus * std::max(1, std::min(per_cu, cap_cu)));
     e = hipMemsetAsync(d_work, 0, (size_t)kGroups * kCounterStride, stream);
     if (e != hipSuccess) return e;
-    LaunchConst* lc = reinterpret_cast<LaunchConst*>(reinterpret_cast<char*>(d_work) + kConstOffset);
-    hipLaunchKernelGGL(make_const_kernel, dim3(1), dim3(64), 0, stream, fp, lc);
     DevScene a0 = s2;
     FrameParams a1 = fp;
-    float* a2 = d_out;
-    unsigned long long* a3 = d_counts;
-    unsigned int* a4 = d_work;
-    const LaunchConst* a5 = lc;
+    LaunchConst a2 = make_const(fp);
+    float* a3 = d_out;
+    unsigned long long* a4 = d_counts;
+    unsigned int* a5 = d_work;
     void* args[] = {&a0, &a1, &a2, &a3, &a4, &a5};
     e = hipLaunchKernel(fn, dim3((unsigned)grid), dim3(block), args, lds, stream);
     if (e != hipSuccess) return e;

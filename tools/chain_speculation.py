@@ -109,7 +109,9 @@ def main():
         got = np.clip(acc / np.float32(spp), 0, 1).astype(np.float32)
         ref = O.render(osc, cam, env, npix, spp, mb, row0=i // W_, row_step=npix).reshape(-1, 3)[i % W_]
         assert np.array_equal(got, ref), i
-    ser = np.array([sum(max(int(nr[D // 2]), 1) for D in chain(nd, spp)) for _, _, nd, nr in tr])
+    # the serial chain as the product traces it: a sample that draws nothing repeats for the rest of the
+    # pixel and is traced once (fixed_point), so every distinct offset is counted once
+    ser = np.array([sum(max(int(nr[D // 2]), 1) for D in set(chain(nd, spp))) for _, _, nd, nr in tr])
     mus = np.array([chain(nd, spp + 1)[-1] / spp for _, _, nd, _ in tr])
     print(f"{name}: {npx} pixels, draws/sample mean {mus.mean():.2f} (std {mus.std():.2f}); serial chain "
           f"mean {ser.mean():.1f} rays, max {ser.max()}")

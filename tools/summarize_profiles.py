@@ -1,6 +1,11 @@
-"""Summarise the rocprofv3 output of tools/run_profiles.sh into profiles/ (committed evidence).
+"""Summarise rocprofv3 passes of bench.py into profiles/ (committed evidence).
 
-    python tools/summarize_profiles.py gpurun_out/prof_C2 TAG WORKLOAD [FRAMES]
+    python tools/summarize_profiles.py gpurun_out/SESSION:CFG TAG WORKLOAD [FRAMES]
+        the kt / pmc steps of tools/gpu_session.py (gpurun_out/SESSION_kt_CFG, SESSION_pmc_CFG_GROUP)
+    python tools/summarize_profiles.py DIR TAG WORKLOAD [FRAMES]
+        DIR/kt, DIR/fetch, DIR/write, DIR/req, DIR/sq (one pass each)
+FRAMES (bench warmup + steps) is required when several render-kernel instantiations ran (two-pass
+launches), since a frame is then several dispatches.
 
 Writes profiles/TAG_kernel_stats_WORKLOAD.csv (the --stats table of the kernel-trace run) and
 profiles/TAG_pmc_WORKLOAD.json: per-launch means of every counter of the render kernel, and
@@ -29,7 +34,8 @@ import sys
 import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-KERNEL = r"render(_resume)?_kernel<(0, )?false, false"  # FAST, uninstrumented (any variant)
+# FAST, uninstrumented (any variant): the megakernels and the wavefront kernel
+KERNEL = r"render(_resume)?_kernel<(0, )?false, false|wave_kernel<false"
 
 
 def _rows(pattern):
@@ -45,10 +51,15 @@ def main(prof, tag, workload, frames=None, kernel=KERNEL):
     dispatches of the render kernel (two-pass launches, option "pilot"); every *_per_launch value and
     kernel_avg_ms are then per frame (totals / frames).  Default: one dispatch per frame."""
     os.makedirs(os.path.join(ROOT, "profiles"), exist_ok=True)
-    stats = glob.glob(os.path.join(prof, "kt", "*kernel_stats.csv"))
+    if ":" in prof:   # tools/gpu_session.py layout
+        pre, cfg = prof.split(":")
+        where = {"kt": f"{pre}_kt_{cfg}", **{g: f"{pre}_pmc_{cfg}_{g}" for g in ("fetch", "write", "dram", "req", "sq")}}
+    else:
+        where = {g: os.path.join(prof, g) for g in ("kt", "fetch", "write", "dram", "req", "sq")}
+    stats = glob.glob(os.path.join(where["kt"], "*kernel_stats.csv"))
     if not stats:   # a run that never produced its kernel trace must not overwrite committed summaries
-        sys.exit(f"no kernel trace under {prof}/kt")
-    s = {"workload": workload, "kernel": kernel, "source": "rocprofv3 (tools/run_profiles.sh)"}
+        sys.exit(f"no kernel trace under {where['kt']}")
+    s = {"workload": workload, "kernel": kernel, "source": "rocprofv3 (tools/gpu_session.py kt / pmc steps)"}
     if stats:
         # every instantiation of the render kernel counts (two-pass launches: pass 1 and pass 2; a
         # device-chosen team size launches the other sizes' instantiations, which return at once)
@@ -59,6 +70,8 @@ def main(prof, tag, workload, frames=None, kernel=KERNEL):
                 names.append(r["Name"][:120])
                 calls += int(r["Calls"])
                 total += float(r["TotalDurationNs"])
+        if len(names) > 1 and not frames:
+            sys.exit(f"{len(names)} render-kernel instantiations matched: give FRAMES (frames the run rendered)")
         if names:
             s["kernel_name"] = names[0] if len(names) == 1 else names
             s["kernel_calls"] = calls
@@ -66,7 +79,7 @@ def main(prof, tag, workload, frames=None, kernel=KERNEL):
             s["kernel_avg_ms"] = total / 1e6 / s["frames"]
     counters = {}
     for sub in ("fetch", "write", "dram", "req", "sq"):
-        for r in _rows(os.path.join(prof, sub, "*counter_collection.csv")):
+        for r in _rows(os.path.join(where[sub], "*counter_collection.csv")):
             if re.search(kernel, r["Kernel_Name"]):
                 counters.setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))
     nframes = max(1, s.get("frames", 1))
