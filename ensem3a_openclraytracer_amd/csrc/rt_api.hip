@@ -30,6 +30,8 @@
 // lanes still rendering: 36 on the BVH2 walk (C3 / C4 ms at 32 / 36 / 40: 138.8 / 136.8 / 136.5,
 // 446.8 / 452.6 / 455.0), 48 on the 4-wide walk (C5 at 40 / 48 / 52: 5,805 / 5,705 / 5,772)
 constexpr int kResumeMinBvh2 = 36, kResumeMinWide = 48;
+// wavefront trace phase: a refill of the idle lanes once this many are idle (option "wf_refill")
+constexpr int kWfRefillAuto = 16;
 #ifndef RT_BRUTE_MAX_DEFAULT
 #define RT_BRUTE_MAX_DEFAULT 64   // FAST tests every triangle of scenes up to this size (rt_set_option "brute_max")
 #endif
@@ -112,6 +114,7 @@ struct rt_ctx {
     int stack_lds = 0;    // FAST stack entries per lane kept in LDS (0 = auto: rt::kStackLds, kStackLdsWide)
     int wavefront = -1;   // tree walk split into trace / shade phases: path slots per lane (0 = off, -1 = auto)
     int ref_stack = 20;   // REF traversal stack capacity (20 = the reference's, stack.cl:4)
+    int wf_refill = 0;    // wavefront trace phase: idle lanes that trigger a refill (0 = auto)
     std::string err;
 };
 
@@ -705,6 +708,7 @@ int check_frame(rt_ctx* ctx, const float* cam, const float* env, int64_t npix, i
     fp->max_waves = ctx->max_waves;
     fp->wf_slots = ctx->wavefront > 0 ? ctx->wavefront : (ctx->wavefront < 0 ? auto_wavefront(ctx, *fp) : 0);
     fp->wf_buf = nullptr;
+    fp->wf_refill = ctx->wf_refill > 0 ? ctx->wf_refill : kWfRefillAuto;
     fp->log_buf = nullptr;
     fp->log_cap = 0;
     fp->log_count = nullptr;
@@ -889,6 +893,11 @@ int rt_set_option(rt_ctx* ctx, const char* key, int64_t value) {
     if (!std::strcmp(key, "ref_stack")) {
         if (value < 20 || value > 64) return set_err(ctx, RT_ERR_ARG, "ref_stack must be in 20..64 (20 = the reference's)");
         ctx->ref_stack = (int)value;
+        return RT_OK;
+    }
+    if (!std::strcmp(key, "wf_refill")) {
+        if (value < 0 || value > 64) return set_err(ctx, RT_ERR_ARG, "wf_refill must be 0 (auto) or 1..64");
+        ctx->wf_refill = (int)value;
         return RT_OK;
     }
     if (!std::strcmp(key, "wavefront")) {

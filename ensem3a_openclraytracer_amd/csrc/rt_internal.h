@@ -138,6 +138,7 @@ struct FrameParams {
     // lane (0: the per-lane megakernel); wf_buf: the per-wave regions (wavefront_bytes)
     int32_t wf_slots;
     float* wf_buf;
+    int32_t wf_refill;   // trace phase: idle lanes that trigger a refill from the wave's ray queue (1..64)
     // debug event log of one pixel (rt_debug_pixel_log only; unused by the product launches)
     int64_t log_pixel;
     float* log_buf;

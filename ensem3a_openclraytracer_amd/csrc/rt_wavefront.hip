@@ -25,6 +25,8 @@
 // are unchanged and frames are bit-identical to the megakernel's (and, through it, to the oracle).
 // Paths are compacted in place (a live path moves to a queue position <= its old one), so the state
 // rows of paths that did not move are rewritten only where they changed.
+#include <cstddef>
+
 #include "rt_device.h"
 
 namespace rt {
@@ -74,12 +76,27 @@ struct WfArgs {
     FrameParams F;
     LaunchConst C;
 };
+// the kernel argument segment puts each argument at the next offset of its alignment: the same offsets
+// as WfArgs (checked against the code object's argument metadata by tests/test_native_abi.py)
+constexpr size_t wf_align(size_t x, size_t a) { return (x + a - 1) / a * a; }
+static_assert(offsetof(WfArgs, F) == wf_align(sizeof(DevScene), alignof(FrameParams)), "kernarg layout");
+static_assert(offsetof(WfArgs, C) == wf_align(offsetof(WfArgs, F) + sizeof(FrameParams), alignof(LaunchConst)),
+              "kernarg layout");
 
 // RT_WF_OPAQUE: the parameters are re-read (scalar loads from the kernel argument segment, through a
 // pointer the compiler cannot see through) at the start of every shade sub-round and trace phase, so
 // that the values only one phase uses are not held in SGPRs across the other (SGPR spills into VGPR lanes)
 #ifndef RT_WF_OPAQUE
 #define RT_WF_OPAQUE 1
+#endif
+// RT_WF_PREFETCH: each lane of the trace phase holds its next queued ray's record, loaded while it traces
+// (8 VGPRs more); otherwise idle lanes are refilled in batches (FrameParams::wf_refill)
+#ifndef RT_WF_PREFETCH
+#define RT_WF_PREFETCH 0
+#endif
+// RT_WF_PK: the 4-wide node's slabs in packed FP32 (rt_device.h wide_node PK)
+#ifndef RT_WF_PK
+#define RT_WF_PK 0
 #endif
 #if RT_WF_OPAQUE
 typedef const char __attribute__((address_space(4))) kernarg_char;
@@ -398,9 +415,46 @@ wave_kernel(DevScene S, FrameParams F, LaunchConst C, float* __restrict__ out, u
         bool tracing = false;
         unsigned myq = 0;
         unsigned next = 0;   // queue entries handed out (wave-uniform)
+#if RT_WF_PREFETCH
+        // every lane keeps one claimed queue entry whose ray record is loaded while it traces the current
+        // ray: a lane whose ray is done starts the next one with no memory round trip of its own
+        bool have = false;
+        float4 pa = make_float4(0, 0, 0, 0), pb = make_float4(0, 0, 0, 0);
+        unsigned pq_ = 0;
+#endif
         while (true) {
+#if RT_WF_PREFETCH
+            if (!tracing && have) {   // start the prefetched ray (its record was loaded during earlier steps)
+                myq = pq_;
+                have = false;
+                const bool sun = as_i(pb.z) != 0;
+                tracing = !fast_init<COUNT>(S, T, rtm_v3(pa.x, pa.y, pa.z), sun ? C.sun : rtm_v3(pa.w, pb.x, pb.y), c);
+                if (WIDE) T.item = S.wroot_ref;
+                T.any = sun && F.sun_any != 0;
+                if (!tracing) hb[myq] = make_float2(T.bk, as_f(-1));
+            }
+            const unsigned long long want = __ballot(!have);
+            if (want && next < n) {   // claim the next entries and issue their loads (not waited for here)
+                const unsigned qq = lane_prefix(want, next);
+                if (!have && qq < n) {
+                    pq_ = qq;
+                    pa = rb0[qq];
+                    pb = rb1[qq];
+                    have = true;
+                }
+                next += (unsigned)__popcll(want);
+            }
+            if (!__any(tracing)) {
+                if (!__any(have)) break;
+                continue;
+            }
+#else
+            // refill the idle lanes from the queue once at least F.wf_refill of them are idle (a refill costs
+            // the wave a memory round trip for the rays before their first step), or when the queue's
+            // rest fits them, or when no lane traces
             const unsigned long long idle = __ballot(!tracing);
-            if (idle && next < n) {
+            const unsigned ni = (unsigned)__popcll(idle);
+            if (idle && next < n && (ni >= (unsigned)F.wf_refill || n - next <= ni || ni == 64u)) {
                 const unsigned qq = lane_prefix(idle, next);
                 if (!tracing && qq < n) {
                     myq = qq;
@@ -417,8 +471,9 @@ wave_kernel(DevScene S, FrameParams F, LaunchConst C, float* __restrict__ out, u
                 if (next >= n) break;
                 continue;
             }
+#endif
             if (tracing) {
-                const bool done = WIDE ? wide_step<COUNT, OVF>(T, nb, tb, lst, c)
+                const bool done = WIDE ? wide_step<COUNT, OVF, RT_WF_PK != 0>(T, nb, tb, lst, c)
                                        : fast_step<COUNT, false, OVF>(S, T, nb, tb, lst, 16u, c);
                 if (done) {
                     tracing = false;
