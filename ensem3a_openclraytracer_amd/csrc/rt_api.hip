@@ -53,6 +53,7 @@ struct Device {
     DevBuf nodes, wnodes, wleaves, tri_fast, brute, brute_box, bvh9, tri_geo, tri_shade, tri_frame, mat, ibl, out, out8, counts, work, scratch_a, scratch_b;
     DevBuf pilot;                 // two-pass launches: per-pixel state, cost and order (FrameParams::pilot_*)
     DevBuf wf;                    // wavefront launches: the waves' path-state regions (FrameParams::wf_buf)
+    DevBuf spec;                  // speculation: the trails' sample logs (FrameParams::spec_log)
     char* host_stage = nullptr;   // pinned staging for rt_render / rt_render_rgb8
     size_t host_stage_bytes = 0;
     // Every launch of this context on the device shares `work` (pixel counters + launch constants)
@@ -115,6 +116,7 @@ struct rt_ctx {
     int wavefront = -1;   // tree walk split into trace / shade phases: path slots per lane (0 = off, -1 = auto)
     int ref_stack = 20;   // REF traversal stack capacity (20 = the reference's, stack.cl:4)
     int wf_refill = 0;    // wavefront trace phase: idle lanes that trigger a refill (0 = auto)
+    int spec = -1;        // small tiles: speculative trails per pixel in pass 2 (0 = off, 2 or 4, -1 = auto)
     std::string err;
 };
 
@@ -700,6 +702,10 @@ int check_frame(rt_ctx* ctx, const float* cam, const float* env, int64_t npix, i
     fp->pilot_chunk = 1;
     fp->pilot_levels = 256;
     fp->pilot_state = nullptr;
+    fp->pilot_draws = nullptr;
+    fp->spec = 0;
+    fp->spec_log = nullptr;
+    fp->spec_cap = 0;
     fp->walk_team_dev = nullptr;
     fp->pilot_cost = nullptr;
     fp->pilot_order = nullptr;
@@ -767,7 +773,7 @@ void rt_destroy(rt_ctx* ctx) {
         if (d.pending) (void)hipEventSynchronize(d.done);
         if (d.stream) (void)hipStreamSynchronize(d.stream);
         for (DevBuf* b : {&d.stack_ovf, &d.nodes, &d.wnodes, &d.wleaves, &d.tri_fast, &d.brute, &d.brute_box, &d.bvh9, &d.tri_geo, &d.tri_shade, &d.tri_frame, &d.mat, &d.ibl, &d.out,
-                          &d.out8, &d.counts, &d.work, &d.scratch_a, &d.scratch_b, &d.pilot, &d.wf})
+                          &d.out8, &d.counts, &d.work, &d.scratch_a, &d.scratch_b, &d.pilot, &d.wf, &d.spec})
             release(*b);
         if (d.host_stage) (void)hipHostFree(d.host_stage);
         if (d.stream) (void)hipStreamDestroy(d.stream);
@@ -893,6 +899,12 @@ int rt_set_option(rt_ctx* ctx, const char* key, int64_t value) {
     if (!std::strcmp(key, "ref_stack")) {
         if (value < 20 || value > 64) return set_err(ctx, RT_ERR_ARG, "ref_stack must be in 20..64 (20 = the reference's)");
         ctx->ref_stack = (int)value;
+        return RT_OK;
+    }
+    if (!std::strcmp(key, "spec")) {
+        if (value != -1 && value != 0 && value != 2 && value != 4)
+            return set_err(ctx, RT_ERR_ARG, "spec must be -1 (auto), 0 (off), 2 or 4");
+        ctx->spec = (int)value;
         return RT_OK;
     }
     if (!std::strcmp(key, "wf_refill")) {
@@ -1081,9 +1093,10 @@ hipError_t setup_pilot(rt_ctx* ctx, Device& d, rt::FrameParams& fp) {
     if (k >= fp.spp) return hipSuccess;
     const size_t n = (size_t)fp.nloc;
     // state 32 B | cost 4 B | order 4 B per pixel, bin totals + offsets (2 x 256), the chunk costs +
-    // chunk order (at most one chunk per pixel) and the sort's segment histograms (256 per 256 chunks)
+    // chunk order (at most one chunk per pixel), the sort's segment histograms (256 per 256 chunks) and
+    // each pixel's pass-1 RNG offset (4 B, pilot_draws)
     const size_t need = n * 40 + 2 * 256 * sizeof(uint32_t) + 2 * (n + 1) * sizeof(uint32_t) +
-                        (n + 256) * sizeof(uint32_t);
+                        (n + 256) * sizeof(uint32_t) + n * sizeof(uint32_t);
     hipError_t e = hipSuccess;
     // growing frees the old buffer from the host: the last launch (any stream) may still use it
     if (d.pilot.bytes < need && d.pending) e = hipEventSynchronize(d.done);
@@ -1096,6 +1109,19 @@ hipError_t setup_pilot(rt_ctx* ctx, Device& d, rt::FrameParams& fp) {
     fp.pilot_state = (float4*)base;
     fp.pilot_cost = (uint32_t*)(base + n * 32);
     fp.pilot_order = (const uint32_t*)(base + n * 36);
+    fp.pilot_draws = (uint32_t*)(base + need - n * sizeof(uint32_t));
+    // speculation (option "spec"): small tiles of the BVH2 walk continue as trails in pass 2
+    const int64_t lanes = (int64_t)std::max(d.cus, 1) * 1024;   // the BVH2 walk's 4 waves per SIMD
+    const int trails = ctx->spec > 0 ? ctx->spec : 0;
+    if (trails > 0 && fp.nloc <= lanes && !use_wide(ctx) && ctx->hs.nbrute == 0) {
+        fp.spec = trails;
+        fp.spec_cap = fp.spp;
+        const size_t lbytes = rt::spec_log_bytes(fp);
+        if (d.spec.bytes < lbytes && d.pending) e = hipEventSynchronize(d.done);
+        if (e == hipSuccess) e = ensure(d.spec, lbytes);
+        if (e != hipSuccess) return e;
+        fp.spec_log = (float4*)d.spec.p;
+    }
     return hipSuccess;
 }
 }  // namespace

@@ -132,6 +132,12 @@ struct FrameParams {
     int32_t pilot_levels;  // cost bins of the order (2..256); within a bin the chunks keep tile order
     float4* pilot_state;
     uint32_t* pilot_cost;
+    uint32_t* pilot_draws;   // BVH2 walk: random numbers each pixel drew in pass 1 (its RNG offset at pilot_state)
+    // Pass 2 with sample-parallel speculation (rt_spec.hip, option "spec"): spec trails per pixel, each
+    // trail's log of (RNG offset, sample colour) records, spec_cap records per trail
+    int32_t spec;
+    float4* spec_log;
+    int32_t spec_cap;
     const uint32_t* pilot_order;
     // Wavefront launches (rt_wavefront.hip, option "wavefront"): the tree walk split into a trace phase
     // and a shade phase per wave, every path's state in HBM between them.  wf_slots = path slots per
@@ -160,6 +166,12 @@ bool wavefront_eligible(const DevScene& sc, const FrameParams& fp);
 size_t wavefront_bytes(const DevScene& sc, const FrameParams& fp, int block);
 hipError_t launch_wavefront(const DevScene& sc, const FrameParams& fp, int block, float* d_out,
                             unsigned long long* d_counts, unsigned int* d_work, hipStream_t stream);
+// Sample-parallel speculation (rt_spec.hip): pass 2 of a pilot launch of the BVH2 walk with fp.spec
+// trails per pixel; spec_log_bytes = the size of fp.spec_log it needs
+size_t spec_log_bytes(const FrameParams& fp);
+hipError_t launch_spec(const DevScene& sc, const FrameParams& fp, int block, float* d_out, unsigned int* d_work,
+                       hipStream_t stream);
+bool spec_walk(const DevScene& sc, const FrameParams& fp);
 // test hooks
 hipError_t launch_debug_math(int fn, const float* x, const float* y, float* out, int64_t n, hipStream_t stream);
 hipError_t launch_debug_log(const DevScene& sc, const FrameParams& fp, int traversal, float* d_out,

@@ -436,6 +436,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WIDE ?
     int s = 0;
     bool drew = false;   // the current sample has drawn random numbers (a diffuse or glossy bounce)
     int cost = 0;        // pass 1: rays this pixel traced (pilot_cost)
+    int ndraw = 0;       // pass 1, BVH2 walk: random numbers the pixel drew (its RNG offset, pilot_draws)
     // The deterministic prefix of the pixel's samples (FrameParams::fixed_point; BVH2 walk): a sample's
     // path up to its first diffuse or glossy bounce draws no random number -- it is the cached camera
     // hit followed by straight-through glass bounces (Raytracing.cl:72-77) -- so it is the same path in
@@ -466,6 +467,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WIDE ?
         F.pilot_state[2 * (int64_t)p + 1] =
             make_float4(__uint_as_float(seed0), __uint_as_float(seed1), __int_as_float(tc), __int_as_float(s));
         F.pilot_cost[p] = s >= spp ? 0u : (unsigned)cost;
+        if (!WIDE && F.pilot_draws) F.pilot_draws[p] = (uint32_t)ndraw;
     };
     auto finish_sample = [&]() __attribute__((always_inline)) {  // output += baseColor; next sample from the cached camera hit
         if (LOG && logme) log_event(F, 3.0f, s + 1, rtm_v3(0, 0, 0), rtm_v3(0, 0, 0), 0.0f, 0, so);
@@ -532,6 +534,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WIDE ?
                     acc = rtm_v3(0, 0, 0);
                     s = 0;
                     cost = 0;
+                    ndraw = 0;
                     pre = false;
                     sun_c = SUN_UNKNOWN;
                     phase = PRIMARY;
@@ -664,6 +667,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WIDE ?
                         fdb = SUNC && F.sun_cache && cm.type != 3 && !drew && !F.sun_skip && !(LOG && logme);
                         drew = drew || cm.type != 3;
                         if (cm.type != 3) {   // diffuse (1) or glossy (2): one sampler stream for both
+                            if (!WIDE) ndraw += 2;
                             Bd = hemi_sample(cm.type == 1, n, S.tri_frame[3 * tri], S.tri_frame[3 * tri + 1], f2,
                                              &seed1, &seed0, &invPdf);
                             if (cm.type == 1) brdf = rtm_scale(cm.color, 1.0f / 3.14f);
@@ -1179,6 +1183,9 @@ hipError_t launch_render(const DevScene& sc, const FrameParams& fp, int traversa
     hipLaunchKernelGGL(pilot_expand_kernel, dim3(gp), dim3(256), 0, stream, corder, nfull, chunk, fp.nloc, order);
     FrameParams b = fp;
     b.pass = 2;
+    // small tiles of the BVH2 walk: each pixel's remaining samples as speculative trails (rt_spec.hip)
+    if (traversal == TRAV_FAST && fp.spec > 0 && fp.spec_log && fp.pilot_draws && spec_walk(sc, fp))
+        return launch_spec(sc, b, block, d_out, d_work, stream);
     if (fp.walk_team == 0 && traversal == TRAV_FAST) {
         // pass 2's team size from the pixels pass 1 left unfinished (pilot_team_pick_kernel)
         static_assert(kTeamOffset >= kGroups * kCounterStride && kTeamOffset + 8 <= kConstOffset, "work block layout");
@@ -1196,6 +1203,16 @@ hipError_t launch_render(const DevScene& sc, const FrameParams& fp, int traversa
         b.walk_team_dev = ts;
     }
     return launch_render_pass(sc, b, traversal, block, d_out, nullptr, d_work, stream);
+}
+
+// the launches whose FAST walk is the BVH2 item-step resumable kernel (launch_fast's choice), the walk
+// rt_spec.hip continues
+bool spec_walk(const DevScene& sc, const FrameParams& fp) {
+    const size_t scene_bytes = (size_t)(kNodeF4 * sc.nnodes + 3 * sc.ntri) * sizeof(float4);
+    const bool smem = sc.ntri > 0 && sc.nbrute == 0 && scene_bytes <= kLdsSceneMax;
+    const bool resume = sc.ntri > 0 && sc.nbrute == 0 && fp.resume_min > 0;
+    const bool step = fp.step == 1 || (fp.step == 0 && (size_t)sc.nnodes * kNodeF4 * 16 <= kStepMaxBytes);
+    return resume && !smem && step && !(fp.wide && sc.wnodes);
 }
 
 hipError_t launch_render_pass(const DevScene& sc, const FrameParams& fp, int traversal, int block, float* d_out,

@@ -1069,3 +1069,57 @@ def test_team_walk_steals_across_the_lds_cap(kl):
         kl.native.set_option("walk_team", 0)
         kl.native.set_option("stack_lds", 0)
         kl.native.set_option("bvh_width", 0)
+
+
+@pytest.mark.parametrize("case", ["monkey_c3_64_s4", "serre_96x54_s4", "proto_64_s4", "furnace_64_s4"])
+def test_speculative_trails_render_identically(kl, case):
+    """spec T: on a small tile, pass 2 of the pilot launch runs each pixel's remaining samples as T trails
+    -- trail 0 from the pass-1 state, the others from guessed RNG offsets -- stitched where they meet.
+    The chain's colours are added in the serial order, so the frame is the one-lane frame and the
+    oracle's, bit for bit, whatever the guesses (16 samples, a 2-sample pilot)."""
+    sc, cam, env, npix, _, mb, ibl = W.PARITY_CASES[case].inputs()
+    spp = 16
+    want = _oracle(sc, cam, env, npix, spp, mb, ibl)
+    kl.native.set_option("brute_max", 0)
+    kl.native.set_option("bvh_width", 2)
+    try:
+        frames = {}
+        for trails in (0, 2, 4):
+            kl.native.set_option("spec", trails)
+            for pilot in (2, 5):
+                kl.native.set_option("pilot", pilot)
+                frames[trails, pilot] = _launch(kl, sc, cam, env, npix, spp, mb, ibl, "fast")
+    finally:
+        kl.native.set_option("spec", -1)
+        kl.native.set_option("pilot", -1)
+        kl.native.set_option("bvh_width", 0)
+        kl.native.set_option("brute_max", 64)
+    for key, f in frames.items():
+        np.testing.assert_array_equal(f, want, err_msg=str(key))
+    with pytest.raises(_native.NativeError, match="spec"):
+        kl.native.set_option("spec", 3)
+
+
+@pytest.mark.parametrize("config,row0,step", [("C3", 3, 8), ("C4", 5, 8)])
+def test_speculative_trails_row_tiles(kl, config, row0, step):
+    """A 1/8 row tile of the full-size C3 / C4 frame (the multi-GPU regime) at 64 spp with the automatic
+    small-tile pilot: 2 and 4 trails per pixel give the one-lane tile bit for bit."""
+    import torch
+    from ensem3a_openclraytracer_amd import distributed as D
+    sc, cam, env, npix, _, mb, ibl = W.CONFIGS[config].inputs()
+    spp = 64
+    _launch(kl, sc, cam, env, npix, 1, mb, ibl, "fast")   # uploads the scene and IBL
+    ctx = kl.native
+    width = int(cam[6])
+    out = torch.empty(3 * width * D.tile_rows(npix, width, row0, step), dtype=torch.float32, device="cuda")
+    frames = []
+    try:
+        for trails in (0, 2, 4):
+            ctx.set_option("spec", trails)
+            ctx.render_device(cam, env, npix, spp, mb, row0, step, out.data_ptr())
+            torch.cuda.synchronize()
+            frames.append(out.cpu().numpy().copy())
+    finally:
+        ctx.set_option("spec", -1)
+    for f in frames[1:]:
+        np.testing.assert_array_equal(f, frames[0])
