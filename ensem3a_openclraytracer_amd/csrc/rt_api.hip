@@ -117,6 +117,7 @@ struct rt_ctx {
     int ref_stack = 20;   // REF traversal stack capacity (20 = the reference's, stack.cl:4)
     int wf_refill = 0;    // wavefront trace phase: idle lanes that trigger a refill (0 = auto)
     int spec = -1;        // small tiles: speculative trails per pixel in pass 2 (0 = off, 2 or 4, -1 = auto)
+    int handout = -1;     // pixel hand-out: 0 = interleaved chunks, 1 = a contiguous block per XCD group, -1 = auto
     std::string err;
 };
 
@@ -712,6 +713,7 @@ int check_frame(rt_ctx* ctx, const float* cam, const float* env, int64_t npix, i
     fp->team = ctx->team;
     fp->walk_team = ctx->walk_team;
     fp->max_waves = ctx->max_waves;
+    fp->handout = ctx->handout > 0 ? 1 : 0;
     fp->wf_slots = ctx->wavefront > 0 ? ctx->wavefront : (ctx->wavefront < 0 ? auto_wavefront(ctx, *fp) : 0);
     fp->wf_buf = nullptr;
     fp->wf_refill = ctx->wf_refill > 0 ? ctx->wf_refill : kWfRefillAuto;
@@ -899,6 +901,11 @@ int rt_set_option(rt_ctx* ctx, const char* key, int64_t value) {
     if (!std::strcmp(key, "ref_stack")) {
         if (value < 20 || value > 64) return set_err(ctx, RT_ERR_ARG, "ref_stack must be in 20..64 (20 = the reference's)");
         ctx->ref_stack = (int)value;
+        return RT_OK;
+    }
+    if (!std::strcmp(key, "handout")) {
+        if (value < -1 || value > 1) return set_err(ctx, RT_ERR_ARG, "handout must be -1 (auto), 0 or 1");
+        ctx->handout = (int)value;
         return RT_OK;
     }
     if (!std::strcmp(key, "spec")) {

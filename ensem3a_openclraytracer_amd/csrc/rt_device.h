@@ -812,16 +812,22 @@ enum Phase { FETCH = 0, PRIMARY = 1, PREP = 2, BOUNCE = 3, SUN = 4, DONE = 5 };
 // block runs on.
 struct PixelQueue {
     unsigned dry = 0;   // bit g: group g's counter is exhausted
+    // FrameParams::handout = 1: group g owns the contiguous pixels [g per, (g + 1) per) of the tile instead
+    // of every kGroups-th chunk, so one XCD's rays in flight come from one region of the image (the tree's
+    // lines they need are fewer: the L2 of an XCD holds more of them).  0: interleaved chunks.
+    unsigned per = 0;
 };
 
-// group g's j-th pixel (chunks g, g + kGroups, g + 2 kGroups, ...: increasing in j)
-__device__ __forceinline__ unsigned group_pixel(unsigned g, unsigned j) {
+// group g's j-th pixel (chunks g, g + kGroups, g + 2 kGroups, ...: increasing in j; or the j-th of its block)
+__device__ __forceinline__ unsigned group_pixel(unsigned g, unsigned j, unsigned per) {
+    if (per) return g * per + j;
     constexpr unsigned m = (1u << kChunkShift) - 1u;
     return (((j >> kChunkShift) * (unsigned)kGroups + g) << kChunkShift) | (j & m);
 }
 
 // pixels of group g in a tile of nloc pixels (wave-uniform)
-__device__ __forceinline__ unsigned group_pixels(unsigned g, unsigned nloc) {
+__device__ __forceinline__ unsigned group_pixels(unsigned g, unsigned nloc, unsigned per) {
+    if (per) return g * per >= nloc ? 0u : min(per, nloc - g * per);
     const unsigned chunks = nloc >> kChunkShift, rem = nloc & ((1u << kChunkShift) - 1u);
     const unsigned full = chunks > g ? (chunks - 1u - g) / (unsigned)kGroups + 1u : 0u;
     return (full << kChunkShift) + (chunks % (unsigned)kGroups == g ? rem : 0u);
@@ -846,9 +852,9 @@ __device__ __forceinline__ unsigned take_pixel(PixelQueue& Q, unsigned long long
         unsigned got = 0;
         if (lane == leader) got = atomicAdd(counters + g * (unsigned)(kCounterStride / 4), k);
         const unsigned j0 = (unsigned)__builtin_amdgcn_readfirstlane((int)__shfl(got, leader, 64));
-        const unsigned have = group_pixels(g, nloc);
+        const unsigned have = group_pixels(g, nloc, Q.per);
         const unsigned nok = j0 < have ? min(have - j0, k) : 0u;
-        if (mine && rank >= base && rank < base + nok) q = group_pixel(g, j0 + (rank - base));
+        if (mine && rank >= base && rank < base + nok) q = group_pixel(g, j0 + (rank - base), Q.per);
         if (nok < k) Q.dry |= 1u << g;   // the group's sequence has run past the tile
         base += nok;
     }

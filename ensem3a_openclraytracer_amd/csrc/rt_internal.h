@@ -106,6 +106,7 @@ struct FrameParams {
     int32_t walk_team;   // FAST tree walk (BVH2 item steps): lanes per pixel walking each ray together (1, 2, 4, 8; 0 = auto)
     const int32_t* walk_team_dev;   // pass 2 of a pilot launch with walk_team auto: the team size, chosen on the device
     int32_t max_waves;   // persistent grid: at most this many waves per SIMD (0 = as many as stay resident)
+    int32_t handout;     // pixel hand-out: 0 = chunks interleaved over the XCD groups, 1 = a contiguous block per group
     int32_t step;        // FAST tree walk: 1 = one item per traversal step, 2 = descend-until-leaf rounds, 0 = auto
     // FAST: skip the shadow ray when its result cannot change the sample: envData[3] (sun power) == 0,
     // envData[4] >= 0 and every material colour finite make the sun term of Raytracing.cl:125-137

@@ -67,6 +67,7 @@ spec_kernel(DevScene S, FrameParams F, float* __restrict__ out, unsigned int* __
     int phase = FETCH;
     bool tracing = false;
     PixelQueue pq;
+    pq.per = (F.handout && F.pass != 2) ? (unsigned)((F.nloc + kGroups - 1) / kGroups) : 0u;   // pass 2: cost order, interleaved
     FastRay T;
     T.item = 0; T.soff = 0; T.bk = 1000.0f; T.bt = -1; T.brank = -1; T.any = false;
     T.o = rtm_v3(0, 0, 0); T.d = rtm_v3(0, 0, 1); T.ix = T.iy = T.iz = 0.0f;

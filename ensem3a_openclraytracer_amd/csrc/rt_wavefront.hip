@@ -65,6 +65,35 @@ constexpr unsigned D_P = 1, D_SEED = 2, D_SM = 4, D_KCTC = 8, D_SUNC = 16;
 __device__ __forceinline__ int as_i(float f) { return __float_as_int(f); }
 __device__ __forceinline__ float as_f(int i) { return __int_as_float(i); }
 
+#ifndef RT_WF_NT
+#define RT_WF_NT 0
+#endif
+typedef float wf_f4 __attribute__((ext_vector_type(4)));
+typedef float wf_f2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ float wf_ld(const float* a) { return RT_WF_NT ? __builtin_nontemporal_load(a) : *a; }
+__device__ __forceinline__ float4 wf_ld(const float4* a) {
+    if (!RT_WF_NT) return *a;
+    const wf_f4 v = __builtin_nontemporal_load(reinterpret_cast<const wf_f4*>(a));
+    return make_float4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ float2 wf_ld(const float2* a) {
+    if (!RT_WF_NT) return *a;
+    const wf_f2 v = __builtin_nontemporal_load(reinterpret_cast<const wf_f2*>(a));
+    return make_float2(v.x, v.y);
+}
+__device__ __forceinline__ void wf_st(float* a, float v) {
+    if (RT_WF_NT) __builtin_nontemporal_store(v, a);
+    else *a = v;
+}
+__device__ __forceinline__ void wf_st(float4* a, float4 v) {
+    if (RT_WF_NT) __builtin_nontemporal_store(wf_f4{v.x, v.y, v.z, v.w}, reinterpret_cast<wf_f4*>(a));
+    else *a = v;
+}
+__device__ __forceinline__ void wf_st(float2* a, float2 v) {
+    if (RT_WF_NT) __builtin_nontemporal_store(wf_f2{v.x, v.y}, reinterpret_cast<wf_f2*>(a));
+    else *a = v;
+}
+
 // Every load of a shade sub-round has returned before its first store: a path written to queue
 // position pos may overwrite the row another lane of the wave read at q = pos in this sub-round.
 __device__ __forceinline__ void wait_loads() { __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
@@ -129,10 +158,14 @@ wave_kernel(DevScene S, FrameParams F, LaunchConst C, float* __restrict__ out, u
     float4* const rb0 = reinterpret_cast<float4*>(region + (size_t)SW * 4 * NPL);
     float4* const rb1 = rb0 + SW;
     float2* const hb = reinterpret_cast<float2*>(rb1 + SW);
-    auto P = [&](int f, unsigned q) -> float& { return pl[(unsigned)f * SW + q]; };
+    // state rows, ray records and hits: streamed once per phase, read back one phase later (non-temporal
+    // hints with RT_WF_NT, so the L2 keeps the tree's lines)
+    auto PL = [&](int f, unsigned q) -> float { return wf_ld(&pl[(unsigned)f * SW + q]); };
+    auto PS = [&](int f, unsigned q, float v) { wf_st(&pl[(unsigned)f * SW + q], v); };
 
 
     PixelQueue pq;
+    pq.per = (F.handout && F.pass != 2) ? (unsigned)((F.nloc + kGroups - 1) / kGroups) : 0u;   // pass 2: cost order, interleaved
     unsigned n = SW;     // queue entries (wave-uniform); the first shade phase: every slot takes a pixel
     bool first = true;
     while (true) {
@@ -162,25 +195,25 @@ wave_kernel(DevScene S, FrameParams F, LaunchConst C, float* __restrict__ out, u
             rtm_f3 so = rtm_v3(1, 1, 1);
             rtm_f3 ro = rtm_v3(0, 0, 0), rd = rtm_v3(0, 0, 1);
             if (!first && valid) {
-                const unsigned fl = (unsigned)as_i(P(WF_FL, q));
+                const unsigned fl = (unsigned)as_i(PL(WF_FL, q));
                 phase = (int)(fl & 7u);
                 drew = (fl >> 3) & 1u;
                 fdb = (fl >> 4) & 1u;
                 pre = (fl >> 5) & 1u;
                 j = (int)(fl >> 8);
-                p = as_i(P(WF_P, q));
-                seed0 = (uint32_t)as_i(P(WF_S0, q));
-                seed1 = (uint32_t)as_i(P(WF_S1, q));
-                s = as_i(P(WF_SM, q));
-                tri = as_i(P(WF_TR, q));
-                so = rtm_v3(P(WF_SO, q), P(WF_SO + 1, q), P(WF_SO + 2, q));
-                kc = P(WF_KC, q);
-                tc = as_i(P(WF_TC, q));
-                sun_c = as_i(P(WF_SC, q));
-                const float4 a = rb0[q], b = rb1[q];
+                p = as_i(PL(WF_P, q));
+                seed0 = (uint32_t)as_i(PL(WF_S0, q));
+                seed1 = (uint32_t)as_i(PL(WF_S1, q));
+                s = as_i(PL(WF_SM, q));
+                tri = as_i(PL(WF_TR, q));
+                so = rtm_v3(PL(WF_SO, q), PL(WF_SO + 1, q), PL(WF_SO + 2, q));
+                kc = PL(WF_KC, q);
+                tc = as_i(PL(WF_TC, q));
+                sun_c = as_i(PL(WF_SC, q));
+                const float4 a = wf_ld(&rb0[q]), b = wf_ld(&rb1[q]);
                 ro = rtm_v3(a.x, a.y, a.z);
                 rd = rtm_v3(a.w, b.x, b.y);   // a shadow ray keeps the bounce direction here (its own is C.sun)
-                const float2 h = hb[q];
+                const float2 h = wf_ld(&hb[q]);
                 hk = h.x;
                 ht = as_i(h.y);
             }
@@ -208,11 +241,11 @@ wave_kernel(DevScene S, FrameParams F, LaunchConst C, float* __restrict__ out, u
                 so = rtm_v3(1, 1, 1);
                 drew = false;
                 if (PREFIX && pre) {
-                    tri = as_i(P(WF_PT, q)); j = as_i(P(WF_PJ, q));
-                    so = rtm_v3(P(WF_PSO, q), P(WF_PSO + 1, q), P(WF_PSO + 2, q));
-                    ro = rtm_v3(P(WF_PO, q), P(WF_PO + 1, q), P(WF_PO + 2, q));
-                    rd = rtm_v3(P(WF_PD, q), P(WF_PD + 1, q), P(WF_PD + 2, q));
-                    hk = P(WF_PK, q);
+                    tri = as_i(PL(WF_PT, q)); j = as_i(PL(WF_PJ, q));
+                    so = rtm_v3(PL(WF_PSO, q), PL(WF_PSO + 1, q), PL(WF_PSO + 2, q));
+                    ro = rtm_v3(PL(WF_PO, q), PL(WF_PO + 1, q), PL(WF_PO + 2, q));
+                    rd = rtm_v3(PL(WF_PD, q), PL(WF_PD + 1, q), PL(WF_PD + 2, q));
+                    hk = PL(WF_PK, q);
                 }
             };
             // a sample that drew no random number is every later sample of its pixel (fixed_point)
@@ -304,11 +337,11 @@ wave_kernel(DevScene S, FrameParams F, LaunchConst C, float* __restrict__ out, u
                             // the first bounce of the sample that draws, reached through glass only: its
                             // state goes to the path's row now (read back at every later sample start)
                             pre = true;
-                            P(WF_PJ, q) = as_f(j); P(WF_PT, q) = as_f(tri);
-                            P(WF_PSO, q) = so.x; P(WF_PSO + 1, q) = so.y; P(WF_PSO + 2, q) = so.z;
-                            P(WF_PO, q) = ro.x; P(WF_PO + 1, q) = ro.y; P(WF_PO + 2, q) = ro.z;
-                            P(WF_PD, q) = rd.x; P(WF_PD + 1, q) = rd.y; P(WF_PD + 2, q) = rd.z;
-                            P(WF_PK, q) = hk;
+                            PS(WF_PJ, q, as_f(j)); PS(WF_PT, q, as_f(tri));
+                            PS(WF_PSO, q, so.x); PS(WF_PSO + 1, q, so.y); PS(WF_PSO + 2, q, so.z);
+                            PS(WF_PO, q, ro.x); PS(WF_PO + 1, q, ro.y); PS(WF_PO + 2, q, ro.z);
+                            PS(WF_PD, q, rd.x); PS(WF_PD + 1, q, rd.y); PS(WF_PD + 2, q, rd.z);
+                            PS(WF_PK, q, hk);
                         }
                         fdb = F.sun_cache && cm.type != 3 && !drew && !F.sun_skip;
                         drew = drew || cm.type != 3;
@@ -370,30 +403,30 @@ wave_kernel(DevScene S, FrameParams F, LaunchConst C, float* __restrict__ out, u
             if (live) {
                 const unsigned fl = (unsigned)phase | (drew ? 8u : 0u) | (fdb ? 16u : 0u) | (pre ? 32u : 0u) |
                                     ((unsigned)j << 8);
-                rb0[pos] = make_float4(ro.x, ro.y, ro.z, rd.x);
-                rb1[pos] = make_float4(rd.y, rd.z, as_f(phase == SUN ? 1 : 0), 0.0f);
-                P(WF_FL, pos) = as_f((int)fl);
-                P(WF_TR, pos) = as_f(tri);
-                P(WF_SO, pos) = so.x; P(WF_SO + 1, pos) = so.y; P(WF_SO + 2, pos) = so.z;
-                if (moved || (dirty & D_P)) P(WF_P, pos) = as_f(p);
+                wf_st(&rb0[pos], make_float4(ro.x, ro.y, ro.z, rd.x));
+                wf_st(&rb1[pos], make_float4(rd.y, rd.z, as_f(phase == SUN ? 1 : 0), 0.0f));
+                PS(WF_FL, pos, as_f((int)fl));
+                PS(WF_TR, pos, as_f(tri));
+                PS(WF_SO, pos, so.x); PS(WF_SO + 1, pos, so.y); PS(WF_SO + 2, pos, so.z);
+                if (moved || (dirty & D_P)) PS(WF_P, pos, as_f(p));
                 if (moved || (dirty & D_SEED)) {
-                    P(WF_S0, pos) = as_f((int)seed0);
-                    P(WF_S1, pos) = as_f((int)seed1);
+                    PS(WF_S0, pos, as_f((int)seed0));
+                    PS(WF_S1, pos, as_f((int)seed1));
                 }
-                if (moved || (dirty & D_SM)) P(WF_SM, pos) = as_f(s);
+                if (moved || (dirty & D_SM)) PS(WF_SM, pos, as_f(s));
                 if (moved || (dirty & D_KCTC)) {
-                    P(WF_KC, pos) = kc;
-                    P(WF_TC, pos) = as_f(tc);
+                    PS(WF_KC, pos, kc);
+                    PS(WF_TC, pos, as_f(tc));
                 }
-                if (moved || (dirty & D_SUNC)) P(WF_SC, pos) = as_f(sun_c);
+                if (moved || (dirty & D_SUNC)) PS(WF_SC, pos, as_f(sun_c));
             }
             // a moved path's glass prefix goes to its new row plane by plane: every lane's read of a plane
             // returns before any lane writes that plane (the other planes are not touched in between)
             if (copy_pre) {
                 for (int f = 0; f < 12; ++f) {
-                    const float v = P(WF_PJ + f, q);
+                    const float v = PL(WF_PJ + f, q);
                     wait_loads();
-                    P(WF_PJ + f, pos) = v;
+                    PS(WF_PJ + f, pos, v);
                 }
             }
             nout += (unsigned)__popcll(m);
@@ -431,15 +464,15 @@ wave_kernel(DevScene S, FrameParams F, LaunchConst C, float* __restrict__ out, u
                 tracing = !fast_init<COUNT>(S, T, rtm_v3(pa.x, pa.y, pa.z), sun ? C.sun : rtm_v3(pa.w, pb.x, pb.y), c);
                 if (WIDE) T.item = S.wroot_ref;
                 T.any = sun && F.sun_any != 0;
-                if (!tracing) hb[myq] = make_float2(T.bk, as_f(-1));
+                if (!tracing) wf_st(&hb[myq], make_float2(T.bk, as_f(-1)));
             }
             const unsigned long long want = __ballot(!have);
             if (want && next < n) {   // claim the next entries and issue their loads (not waited for here)
                 const unsigned qq = lane_prefix(want, next);
                 if (!have && qq < n) {
                     pq_ = qq;
-                    pa = rb0[qq];
-                    pb = rb1[qq];
+                    pa = wf_ld(&rb0[qq]);
+                    pb = wf_ld(&rb1[qq]);
                     have = true;
                 }
                 next += (unsigned)__popcll(want);
@@ -458,12 +491,12 @@ wave_kernel(DevScene S, FrameParams F, LaunchConst C, float* __restrict__ out, u
                 const unsigned qq = lane_prefix(idle, next);
                 if (!tracing && qq < n) {
                     myq = qq;
-                    const float4 a = rb0[qq], b = rb1[qq];
+                    const float4 a = wf_ld(&rb0[qq]), b = wf_ld(&rb1[qq]);
                     const bool sun = as_i(b.z) != 0;
                     tracing = !fast_init<COUNT>(S, T, rtm_v3(a.x, a.y, a.z), sun ? C.sun : rtm_v3(a.w, b.x, b.y), c);
                     if (WIDE) T.item = S.wroot_ref;
                     T.any = sun && F.sun_any != 0;
-                    if (!tracing) hb[qq] = make_float2(T.bk, as_f(-1));
+                    if (!tracing) wf_st(&hb[qq], make_float2(T.bk, as_f(-1)));
                 }
                 next += (unsigned)__popcll(idle);
             }
@@ -477,7 +510,7 @@ wave_kernel(DevScene S, FrameParams F, LaunchConst C, float* __restrict__ out, u
                                        : fast_step<COUNT, false, OVF>(S, T, nb, tb, lst, 16u, c);
                 if (done) {
                     tracing = false;
-                    hb[myq] = make_float2(T.bk, as_f(T.bt >= 0 ? (int)((unsigned)T.bt / 48u) : -1));
+                    wf_st(&hb[myq], make_float2(T.bk, as_f(T.bt >= 0 ? (int)((unsigned)T.bt / 48u) : -1)));
                 }
             }
         }

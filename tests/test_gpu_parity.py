@@ -1123,3 +1123,27 @@ def test_speculative_trails_row_tiles(kl, config, row0, step):
         ctx.set_option("spec", -1)
     for f in frames[1:]:
         np.testing.assert_array_equal(f, frames[0])
+
+
+@pytest.mark.parametrize("case", ["cornell_128_s16", "monkey_c3_64_s4", "grid"])
+def test_block_handout_renders_identically(kl, case):
+    """handout 1: each XCD group takes a contiguous block of the tile instead of interleaved chunks --
+    a different assignment of pixels to waves, never a different frame (lock-step brute force, BVH2
+    walk, 4-wide walk and the wavefront walk)."""
+    if case == "grid":
+        sc, cam, env, npix, spp, mb, ibl = W.CONFIGS["C5"].with_size(48, 27, 2).inputs()
+    else:
+        sc, cam, env, npix, spp, mb, ibl = W.PARITY_CASES[case].inputs()
+    want = _oracle(sc, cam, env, npix, spp, mb, ibl)
+    try:
+        for wf in (0, 4):
+            kl.native.set_option("wavefront", wf)
+            for h in (0, 1):
+                kl.native.set_option("handout", h)
+                np.testing.assert_array_equal(_launch(kl, sc, cam, env, npix, spp, mb, ibl, "fast"), want,
+                                              err_msg=f"wavefront {wf} handout {h}")
+    finally:
+        kl.native.set_option("handout", -1)
+        kl.native.set_option("wavefront", -1)
+    with pytest.raises(_native.NativeError, match="handout"):
+        kl.native.set_option("handout", 2)

@@ -34,6 +34,7 @@ LIMITS = {"clock": 30, "pytest": 900, "bench": 300, "benchfull": 600, "smoke": 1
 PMC = {
     "fetch": "FETCH_SIZE",
     "write": "WRITE_SIZE",
+    "hit": "TCC_HIT_sum TCC_MISS_sum TCC_REQ_sum TCC_EA0_WRREQ_64B_sum",
     "req": "TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_128B_sum",
     "sq": "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_THREAD_CYCLES_VALU "
           "SQ_WAIT_ANY SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE GRBM_COUNT",
@@ -76,7 +77,8 @@ def command(kind, val, tag, n):
     if kind in ("kt", "pmc"):
         cfg = p[0]
         opts = (p[2] if len(p) > 2 else "") if kind == "pmc" else (p[1] if len(p) > 1 else "")
-        name = f"{tag}_{kind}_{cfg}" + (f"_{p[1]}" if kind == "pmc" else "")
+        name = f"{tag}_{kind}_{cfg}" + (f"_{p[1]}" if kind == "pmc" else "") + \
+            ("_" + "".join(ch if ch.isalnum() else "-" for ch in opts) if opts else "")
         prof = ["rocprofv3"] + (["--kernel-trace", "--stats"] if kind == "kt" else ["--pmc"] + PMC[p[1]].split())
         return prof + ["--output-format", "csv", "-d", os.path.join(OUT, name), "-o", name, "--"] + \
             bench_args(cfg, "1", "1", opts) + ["--no-counts"], env
