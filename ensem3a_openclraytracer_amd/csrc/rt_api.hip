@@ -1082,7 +1082,7 @@ hipError_t setup_pilot(rt_ctx* ctx, Device& d, rt::FrameParams& fp) {
     if (fp.wf_buf || ctx->pilot == 0 || effective_traversal(ctx) != RT_TRAVERSAL_FAST || fp.nloc <= 0) return hipSuccess;
     int k = ctx->pilot;
     if (k < 0) {   // auto: the tree walk on tiles of 1-16 pixels per resident lane (where the tail is long)
-        const int64_t lanes = (int64_t)std::max(d.cus, 1) * 1280;
+        const int64_t lanes = (int64_t)std::max(d.cus, 1) * rt::kWalkLanesPerCu;
         // not on the 4-wide walk (C5), whose L2-missing walk loses the coherence of neighbouring pixels
         // when they are reordered: r03 row tiles 1/2, 1/4, 1/8: 3,005 / 1,626 / 937 ms without the pilot,
         // 3,185 / 1,694 / 938 with it
@@ -1118,10 +1118,11 @@ hipError_t setup_pilot(rt_ctx* ctx, Device& d, rt::FrameParams& fp) {
     fp.pilot_order = (const uint32_t*)(base + n * 36);
     fp.pilot_draws = (uint32_t*)(base + need - n * sizeof(uint32_t));
     // speculation (option "spec"): small tiles of the BVH2 walk continue as trails in pass 2
-    const int64_t lanes = (int64_t)std::max(d.cus, 1) * 1024;   // the BVH2 walk's 4 waves per SIMD
-    const int trails = ctx->spec > 0 ? ctx->spec : 0;
-    if (trails > 0 && fp.nloc <= lanes && !use_wide(ctx) && ctx->hs.nbrute == 0) {
-        fp.spec = trails;
+    const int64_t lanes = (int64_t)std::max(d.cus, 1) * rt::kWalkLanesPerCu;
+    // up to 4 pixels per resident lane: pass 1 finishes the pixels that draw nothing (sky), and the device
+    // picks trails only when the rest is at most one pixel per lane (pilot_team_pick_kernel)
+    if (ctx->spec != 0 && fp.nloc <= 4 * lanes && !use_wide(ctx) && ctx->hs.nbrute == 0) {
+        fp.spec = ctx->spec;   // 2 or 4 trails, or -1: chosen on the device from the pixels pass 1 left
         fp.spec_cap = fp.spp;
         const size_t lbytes = rt::spec_log_bytes(fp);
         if (d.spec.bytes < lbytes && d.pending) e = hipEventSynchronize(d.done);

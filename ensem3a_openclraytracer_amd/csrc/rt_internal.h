@@ -169,6 +169,12 @@ hipError_t launch_wavefront(const DevScene& sc, const FrameParams& fp, int block
                             unsigned long long* d_counts, unsigned int* d_work, hipStream_t stream);
 // Sample-parallel speculation (rt_spec.hip): pass 2 of a pilot launch of the BVH2 walk with fp.spec
 // trails per pixel; spec_log_bytes = the size of fp.spec_log it needs
+// at most kSpecTrails trails per pixel; a log holds kSpecTrails - 1 trails per pixel whatever the count;
+// the device pick of pass 2 encodes "T trails" as kSpecPick + T in FrameParams::walk_team_dev
+constexpr int kSpecTrails = 4;
+constexpr int kSpecPick = 10;
+// resident lanes per CU of the BVH2 walks (render_resume_kernel, spec_kernel: 4 waves per SIMD)
+constexpr int kWalkLanesPerCu = 4 * 4 * 64;
 size_t spec_log_bytes(const FrameParams& fp);
 hipError_t launch_spec(const DevScene& sc, const FrameParams& fp, int block, float* d_out, unsigned int* d_work,
                        hipStream_t stream);

@@ -781,10 +781,15 @@ __global__ void pilot_team_count_kernel(const uint32_t* __restrict__ cost, int64
     if ((threadIdx.x & 63) == 0 && k) atomicAdd(left, k);
 }
 
-__global__ void pilot_team_pick_kernel(const unsigned* __restrict__ left, int64_t lanes, int* __restrict__ ts) {
+// spec: with speculation available (FrameParams::spec < 0, auto) the same thresholds pick trails instead of
+// teams: 4 trails per pixel at u <= 1/2 per lane, 2 at u <= 1 (r04, 1/8 and 1/4 row tiles: C4 1/8 u ~ 0.23
+// per lane: 4 trails 85 ms, teams 109, 2 trails 137; C3 1/8 u ~ 0.47: 2 / 4 trails 36.1 / 36.2 ms, teams
+// 50.7; C3 1/4 u ~ 0.93: 2 trails 53.8, 4 trails 61.6, teams 66.8), encoded kSpecPick + trails
+__global__ void pilot_team_pick_kernel(const unsigned* __restrict__ left, int64_t lanes, int spec, int* __restrict__ ts) {
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         const int64_t u2 = 2 * (int64_t)*left;   // 2 u lanes
-        *ts = u2 <= lanes ? 4 : u2 <= 2 * lanes ? 2 : 1;
+        const int k = u2 <= lanes ? 4 : u2 <= 2 * lanes ? 2 : 1;
+        *ts = (spec && k > 1) ? kSpecPick + k : k;
     }
 }
 
@@ -1185,9 +1190,10 @@ hipError_t launch_render(const DevScene& sc, const FrameParams& fp, int traversa
     hipLaunchKernelGGL(pilot_expand_kernel, dim3(gp), dim3(256), 0, stream, corder, nfull, chunk, fp.nloc, order);
     FrameParams b = fp;
     b.pass = 2;
-    // small tiles of the BVH2 walk: each pixel's remaining samples as speculative trails (rt_spec.hip)
-    if (traversal == TRAV_FAST && fp.spec > 0 && fp.spec_log && fp.pilot_draws && spec_walk(sc, fp))
-        return launch_spec(sc, b, block, d_out, d_work, stream);
+    // small tiles of the BVH2 walk: each pixel's remaining samples as speculative trails (rt_spec.hip):
+    // a set number of trails, or (spec < 0) chosen on the device with the team size
+    const bool spec_ok = traversal == TRAV_FAST && fp.spec != 0 && fp.spec_log && fp.pilot_draws && spec_walk(sc, fp);
+    if (spec_ok && fp.spec > 0) return launch_spec(sc, b, block, d_out, d_work, stream);
     if (fp.walk_team == 0 && traversal == TRAV_FAST) {
         // pass 2's team size from the pixels pass 1 left unfinished (pilot_team_pick_kernel)
         static_assert(kTeamOffset >= kGroups * kCounterStride && kTeamOffset + 8 <= kConstOffset, "work block layout");
@@ -1201,8 +1207,19 @@ hipError_t launch_render(const DevScene& sc, const FrameParams& fp, int traversa
         hipLaunchKernelGGL(pilot_team_count_kernel, dim3(gp), dim3(256), 0, stream, fp.pilot_cost, fp.nloc, left);
         // resident lanes of the one-lane BVH2 walk: 4 waves per SIMD
         hipLaunchKernelGGL(pilot_team_pick_kernel, dim3(1), dim3(64), 0, stream, left,
-                           (int64_t)std::max(cus, 1) * 4 * 4 * 64, ts);
+                           (int64_t)std::max(cus, 1) * kWalkLanesPerCu, spec_ok ? 1 : 0, ts);
         b.walk_team_dev = ts;
+        if (spec_ok) {
+            // the one-lane walk (the team instantiations return at once: a trail pick is no team size), then
+            // the 2- and 4-trail kernels, of which at most the one picked renders
+            e = launch_render_pass(sc, b, traversal, block, d_out, nullptr, d_work, stream);
+            for (int trails = 2; e == hipSuccess && trails <= kSpecTrails; trails *= 2) {
+                FrameParams t = b;
+                t.spec = trails;
+                e = launch_spec(sc, t, block, d_out, d_work, stream);
+            }
+            return e;
+        }
     }
     return launch_render_pass(sc, b, traversal, block, d_out, nullptr, d_work, stream);
 }

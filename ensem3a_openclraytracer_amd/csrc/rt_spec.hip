@@ -44,6 +44,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4)))
 spec_kernel(DevScene S, FrameParams F, float* __restrict__ out, unsigned int* __restrict__ work_counter,
             const LaunchConst* __restrict__ lconst) {
     static_assert(TR == 2 || TR == 4, "trails per pixel");
+    // trails chosen on the device (pilot_team_pick_kernel): only the instantiation picked renders
+    if (F.walk_team_dev && __builtin_amdgcn_readfirstlane(*F.walk_team_dev) != kSpecPick + TR) return;
     extern __shared__ int lds_stack[];
     Cnt c{};
     const LaunchConst& C = *lconst;
@@ -61,7 +63,7 @@ spec_kernel(DevScene S, FrameParams F, float* __restrict__ out, unsigned int* __
     const bool leader = tau == 0;
     const unsigned long long leaders = TR == 2 ? 0x5555555555555555ull : 0x1111111111111111ull;
     auto log_at = [&](int p, int u, int k) -> float4* {   // record k of trail u (>= 1) of pixel p
-        return F.spec_log + ((size_t)p * (TR - 1) + (size_t)(u - 1)) * (size_t)cap + (size_t)k;
+        return F.spec_log + ((size_t)p * (kSpecTrails - 1) + (size_t)(u - 1)) * (size_t)cap + (size_t)k;
     };
 
     int phase = FETCH;
@@ -412,8 +414,8 @@ const void* spec_fn() {
 }  // namespace
 
 size_t spec_log_bytes(const FrameParams& fp) {
-    if (fp.spec != 2 && fp.spec != 4) return 0;
-    return (size_t)fp.nloc * (size_t)(fp.spec - 1) * (size_t)std::max(fp.spp, 1) * sizeof(float4);
+    if (fp.spec == 0) return 0;
+    return (size_t)fp.nloc * (size_t)(kSpecTrails - 1) * (size_t)std::max(fp.spp, 1) * sizeof(float4);
 }
 
 hipError_t launch_spec(const DevScene& sc, const FrameParams& fp, int block, float* d_out, unsigned int* d_work,
