@@ -780,8 +780,8 @@ FULL_SIZE_FAST = {
     # config: (spp, rows (row0, row_step) or None = whole frame, oracle row, the measured set of
     # non-identical pixels (one MI355X), or None while unmeasured (the test then records it)
     "C3": (256, None, 517, {91029, 156256, 490876, 529159, 856344}),
-    "C4": (512, None, 611, None),
-    "C5": (64, None, 700, None),
+    "C4": (512, None, 611, set()),
+    "C5": (64, None, 700, set()),
     "proto": (100, None, 389, {678387}),
     "furnace": (1000, None, 611, set()),
 }
@@ -818,15 +818,15 @@ def test_full_size_fast_vs_ref_pixel_counts(kl, config):
         for trav in ("ref", "fast"):
             frames[trav] = render(trav)
         diff = np.unique(np.nonzero(frames["fast"] != frames["ref"])[0] // 3)
-        drops = None
         kinds = {"drop": 0, "slab": 0}
         if diff.size:
             r64 = render("ref", 64).reshape(-1, 3)
             same = (r64[diff] == frames["fast"].reshape(-1, 3)[diff]).all(1)
             kinds = {"drop": int(same.sum()), "slab": int((~same).sum())}
-            ctx.set_option("traversal", _native.RT_TRAVERSAL_REF)
-            ctx.set_option("ref_stack", 20)
-            drops = ctx.count_work(cam, env, npix, spp_cfg, mb, row0, step)["stack_drops"]
+        # the reference's silent stack drops on this frame (stack.cl:23-24), counted by the REF walk
+        ctx.set_option("traversal", _native.RT_TRAVERSAL_REF)
+        ctx.set_option("ref_stack", 20)
+        drops = ctx.count_work(cam, env, npix, spp_cfg, mb, row0, step)["stack_drops"]
     finally:
         ctx.set_option("traversal", _native.RT_TRAVERSAL_FAST)
         ctx.set_option("ref_stack", 20)

@@ -57,7 +57,7 @@ def command(kind, val, tag, n):
                "|| echo no smi")
         return ["bash", "-c", smi], env
     if kind == "pytest":
-        a = [PY, "-u", "-m", "pytest", "tests", "-m", "gpu", "-x", "-v", "--timeout", "300", "--timeout-method",
+        a = [PY, "-u", "-m", "pytest", "tests", "-m", "gpu", "-x", "-v", "-rP", "--timeout", "300", "--timeout-method",
              "thread"]
         if val and val != "all":
             a += ["-k", val]
