@@ -1137,11 +1137,7 @@ __device__ __forceinline__ bool team_step(int ts, FastRay& R, unsigned& boff, co
 // k > 1e-4, lowest (k, rank)), so the hit is the same.  Returns true when the ray is finished.
 // The wide node on its loaded data: the hit children sorted by entry distance, the others pushed
 // farthest first.  Returns the nearest hit child, or INT_MIN (pop next).
-// PK: the (lo, hi) pair of each axis in one packed-FP32 register pair (v_pk_fma / v_pk_add / v_pk_mul, half
-// the VALU instructions of the slab); each element rounds exactly like the scalar fma / sub / mul.  The
-// megakernel keeps the scalar form (its walk spilled with the pairs)
-typedef float f2 __attribute__((ext_vector_type(2)));
-template <bool COUNT, bool OVF, bool PK = false>
+template <bool COUNT, bool OVF>
 __device__ __forceinline__ int wide_node(float4 g0, float4 g1, float4 g2, float4 g3, FastRay& R, const LaneStack& st,
                                          Cnt& c, bool on = true) {   // on = false: no child is hit
     const float cull = R.bk * CULL_MARGIN;
@@ -1153,35 +1149,15 @@ __device__ __forceinline__ int wide_node(float4 g0, float4 g1, float4 g2, float4
     const unsigned qhx = __float_as_uint(g2.w), qhy = __float_as_uint(g3.x), qhz = __float_as_uint(g3.y);
     int r[4] = {__float_as_int(g1.x), __float_as_int(g1.y), __float_as_int(g1.z), __float_as_int(g1.w)};
     float t[4];
-    if (PK) {
-        const f2 px = {g0.x, g0.x}, py = {g0.y, g0.y}, pz = {g0.z, g0.z};
-        const f2 sxx = {sx, sx}, syy = {sy, sy}, szz = {sz, sz};
-        const f2 nox = {-R.o.x, -R.o.x}, noy = {-R.o.y, -R.o.y}, noz = {-R.o.z, -R.o.z};
-        const f2 ixx = {R.ix, R.ix}, iyy = {R.iy, R.iy}, izz = {R.iz, R.iz};
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            auto qq = [&](unsigned wl, unsigned wh) -> f2 {
-                return f2{(float)((wl >> (8 * i)) & 255u), (float)((wh >> (8 * i)) & 255u)};
-            };
-            // x + (-o) == x - o exactly: the slab's (b - o) * (1 / d) per element
-            const f2 tx = (__builtin_elementwise_fma(qq(qlx, qhx), sxx, px) + nox) * ixx;
-            const f2 ty = (__builtin_elementwise_fma(qq(qly, qhy), syy, py) + noy) * iyy;
-            const f2 tz = (__builtin_elementwise_fma(qq(qlz, qhz), szz, pz) + noz) * izz;
-            const float tn = fmaxf(fmaxf(fminf(tx.x, tx.y), fminf(ty.x, ty.y)), fminf(tz.x, tz.y));
-            const float tm = fminf(fminf(fmaxf(tx.x, tx.y), fmaxf(ty.x, ty.y)), fmaxf(tz.x, tz.y));
-            t[i] = (on && r[i] != INT_MIN && box_hit(tn, tm, cull)) ? tn : INFINITY;   // misses sort last
-        }
-    } else {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            // p + q * s with q * s exact (s a power of two, q < 256): one correctly rounded fma gives the
-            // builder's p + (q * s) bit for bit
-            auto dq = [&](float pp, unsigned w, float sc) { return fmaf((float)((w >> (8 * i)) & 255u), sc, pp); };
-            float tn, tx;
-            slab(dq(g0.x, qlx, sx), dq(g0.x, qhx, sx), dq(g0.y, qly, sy), dq(g0.y, qhy, sy), dq(g0.z, qlz, sz),
-                 dq(g0.z, qhz, sz), R.o, R.ix, R.iy, R.iz, tn, tx);
-            t[i] = (on && r[i] != INT_MIN && box_hit(tn, tx, cull)) ? tn : INFINITY;   // misses sort last
-        }
+    for (int i = 0; i < 4; ++i) {
+        // p + q * s with q * s exact (s a power of two, q < 256): one correctly rounded fma gives the
+        // builder's p + (q * s) bit for bit
+        auto dq = [&](float pp, unsigned w, float sc) { return fmaf((float)((w >> (8 * i)) & 255u), sc, pp); };
+        float tn, tx;
+        slab(dq(g0.x, qlx, sx), dq(g0.x, qhx, sx), dq(g0.y, qly, sy), dq(g0.y, qhy, sy), dq(g0.z, qlz, sz),
+             dq(g0.z, qhz, sz), R.o, R.ix, R.iy, R.iz, tn, tx);
+        t[i] = (on && r[i] != INT_MIN && box_hit(tn, tx, cull)) ? tn : INFINITY;   // misses sort last
     }
     if (COUNT && on) {
         c.nodes++;
@@ -1232,7 +1208,7 @@ __device__ __forceinline__ bool wide_leaf(float4 g0, float4 g1, float4 g2, float
 // intersected.  Nodes and leaves are both 64 bytes, fetched with the same four 16-byte loads, like
 // fast_step.  The accepted triangles are the binary walk's (own exact leaf box passes, MT hit,
 // k > 1e-4, lowest (k, rank)), so the hit is the same.  Returns true when the ray is finished.
-template <bool COUNT, bool OVF, bool PK = false>
+template <bool COUNT, bool OVF>
 __device__ __forceinline__ bool wide_step(FastRay& R, const char* nb, const char* lb, const LaneStack& st, Cnt& c) {
     const bool node = R.item >= 0;
     const char* p = node ? nb + 64u * (unsigned)R.item : lb + ~(unsigned)R.item;
@@ -1242,7 +1218,7 @@ __device__ __forceinline__ bool wide_step(FastRay& R, const char* nb, const char
     const float4 g3 = *reinterpret_cast<const float4*>(p + 48);
     if (COUNT) count_wave(c.wave_trav);
     // both codes on every lane (a step almost always holds node and leaf lanes), predicated
-    const int nx = wide_node<COUNT, OVF, PK>(g0, g1, g2, g3, R, st, c, node);
+    const int nx = wide_node<COUNT, OVF>(g0, g1, g2, g3, R, st, c, node);
     if (wide_leaf<COUNT>(g0, g1, g2, g3, R, c, !node)) return true;
     if (nx != INT_MIN) {
         R.item = nx;

@@ -65,35 +65,6 @@ constexpr unsigned D_P = 1, D_SEED = 2, D_SM = 4, D_KCTC = 8, D_SUNC = 16;
 __device__ __forceinline__ int as_i(float f) { return __float_as_int(f); }
 __device__ __forceinline__ float as_f(int i) { return __int_as_float(i); }
 
-#ifndef RT_WF_NT
-#define RT_WF_NT 0
-#endif
-typedef float wf_f4 __attribute__((ext_vector_type(4)));
-typedef float wf_f2 __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ float wf_ld(const float* a) { return RT_WF_NT ? __builtin_nontemporal_load(a) : *a; }
-__device__ __forceinline__ float4 wf_ld(const float4* a) {
-    if (!RT_WF_NT) return *a;
-    const wf_f4 v = __builtin_nontemporal_load(reinterpret_cast<const wf_f4*>(a));
-    return make_float4(v.x, v.y, v.z, v.w);
-}
-__device__ __forceinline__ float2 wf_ld(const float2* a) {
-    if (!RT_WF_NT) return *a;
-    const wf_f2 v = __builtin_nontemporal_load(reinterpret_cast<const wf_f2*>(a));
-    return make_float2(v.x, v.y);
-}
-__device__ __forceinline__ void wf_st(float* a, float v) {
-    if (RT_WF_NT) __builtin_nontemporal_store(v, a);
-    else *a = v;
-}
-__device__ __forceinline__ void wf_st(float4* a, float4 v) {
-    if (RT_WF_NT) __builtin_nontemporal_store(wf_f4{v.x, v.y, v.z, v.w}, reinterpret_cast<wf_f4*>(a));
-    else *a = v;
-}
-__device__ __forceinline__ void wf_st(float2* a, float2 v) {
-    if (RT_WF_NT) __builtin_nontemporal_store(wf_f2{v.x, v.y}, reinterpret_cast<wf_f2*>(a));
-    else *a = v;
-}
-
 // Every load of a shade sub-round has returned before its first store: a path written to queue
 // position pos may overwrite the row another lane of the wave read at q = pos in this sub-round.
 __device__ __forceinline__ void wait_loads() { __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
@@ -117,15 +88,6 @@ static_assert(offsetof(WfArgs, C) == wf_align(offsetof(WfArgs, F) + sizeof(Frame
 // that the values only one phase uses are not held in SGPRs across the other (SGPR spills into VGPR lanes)
 #ifndef RT_WF_OPAQUE
 #define RT_WF_OPAQUE 1
-#endif
-// RT_WF_PREFETCH: each lane of the trace phase holds its next queued ray's record, loaded while it traces
-// (8 VGPRs more); otherwise idle lanes are refilled in batches (FrameParams::wf_refill)
-#ifndef RT_WF_PREFETCH
-#define RT_WF_PREFETCH 0
-#endif
-// RT_WF_PK: the 4-wide node's slabs in packed FP32 (rt_device.h wide_node PK)
-#ifndef RT_WF_PK
-#define RT_WF_PK 0
 #endif
 #if RT_WF_OPAQUE
 typedef const char __attribute__((address_space(4))) kernarg_char;
@@ -158,11 +120,9 @@ wave_kernel(DevScene S, FrameParams F, LaunchConst C, float* __restrict__ out, u
     float4* const rb0 = reinterpret_cast<float4*>(region + (size_t)SW * 4 * NPL);
     float4* const rb1 = rb0 + SW;
     float2* const hb = reinterpret_cast<float2*>(rb1 + SW);
-    // state rows, ray records and hits: streamed once per phase, read back one phase later (non-temporal
-    // hints with RT_WF_NT, so the L2 keeps the tree's lines)
-    auto PL = [&](int f, unsigned q) -> float { return wf_ld(&pl[(unsigned)f * SW + q]); };
-    auto PS = [&](int f, unsigned q, float v) { wf_st(&pl[(unsigned)f * SW + q], v); };
-
+    // state rows, ray records and hits: streamed once per phase, read back one phase later
+    auto PL = [&](int f, unsigned q) -> float { return pl[(unsigned)f * SW + q]; };
+    auto PS = [&](int f, unsigned q, float v) { pl[(unsigned)f * SW + q] = v; };
 
     PixelQueue pq;
     pq.per = (F.handout && F.pass != 2) ? (unsigned)((F.nloc + kGroups - 1) / kGroups) : 0u;   // pass 2: cost order, interleaved
@@ -210,10 +170,10 @@ wave_kernel(DevScene S, FrameParams F, LaunchConst C, float* __restrict__ out, u
                 kc = PL(WF_KC, q);
                 tc = as_i(PL(WF_TC, q));
                 sun_c = as_i(PL(WF_SC, q));
-                const float4 a = wf_ld(&rb0[q]), b = wf_ld(&rb1[q]);
+                const float4 a = rb0[q], b = rb1[q];
                 ro = rtm_v3(a.x, a.y, a.z);
                 rd = rtm_v3(a.w, b.x, b.y);   // a shadow ray keeps the bounce direction here (its own is C.sun)
-                const float2 h = wf_ld(&hb[q]);
+                const float2 h = hb[q];
                 hk = h.x;
                 ht = as_i(h.y);
             }
@@ -403,8 +363,8 @@ wave_kernel(DevScene S, FrameParams F, LaunchConst C, float* __restrict__ out, u
             if (live) {
                 const unsigned fl = (unsigned)phase | (drew ? 8u : 0u) | (fdb ? 16u : 0u) | (pre ? 32u : 0u) |
                                     ((unsigned)j << 8);
-                wf_st(&rb0[pos], make_float4(ro.x, ro.y, ro.z, rd.x));
-                wf_st(&rb1[pos], make_float4(rd.y, rd.z, as_f(phase == SUN ? 1 : 0), 0.0f));
+                rb0[pos] = make_float4(ro.x, ro.y, ro.z, rd.x);
+                rb1[pos] = make_float4(rd.y, rd.z, as_f(phase == SUN ? 1 : 0), 0.0f);
                 PS(WF_FL, pos, as_f((int)fl));
                 PS(WF_TR, pos, as_f(tri));
                 PS(WF_SO, pos, so.x); PS(WF_SO + 1, pos, so.y); PS(WF_SO + 2, pos, so.z);
@@ -448,40 +408,7 @@ wave_kernel(DevScene S, FrameParams F, LaunchConst C, float* __restrict__ out, u
         bool tracing = false;
         unsigned myq = 0;
         unsigned next = 0;   // queue entries handed out (wave-uniform)
-#if RT_WF_PREFETCH
-        // every lane keeps one claimed queue entry whose ray record is loaded while it traces the current
-        // ray: a lane whose ray is done starts the next one with no memory round trip of its own
-        bool have = false;
-        float4 pa = make_float4(0, 0, 0, 0), pb = make_float4(0, 0, 0, 0);
-        unsigned pq_ = 0;
-#endif
         while (true) {
-#if RT_WF_PREFETCH
-            if (!tracing && have) {   // start the prefetched ray (its record was loaded during earlier steps)
-                myq = pq_;
-                have = false;
-                const bool sun = as_i(pb.z) != 0;
-                tracing = !fast_init<COUNT>(S, T, rtm_v3(pa.x, pa.y, pa.z), sun ? C.sun : rtm_v3(pa.w, pb.x, pb.y), c);
-                if (WIDE) T.item = S.wroot_ref;
-                T.any = sun && F.sun_any != 0;
-                if (!tracing) wf_st(&hb[myq], make_float2(T.bk, as_f(-1)));
-            }
-            const unsigned long long want = __ballot(!have);
-            if (want && next < n) {   // claim the next entries and issue their loads (not waited for here)
-                const unsigned qq = lane_prefix(want, next);
-                if (!have && qq < n) {
-                    pq_ = qq;
-                    pa = wf_ld(&rb0[qq]);
-                    pb = wf_ld(&rb1[qq]);
-                    have = true;
-                }
-                next += (unsigned)__popcll(want);
-            }
-            if (!__any(tracing)) {
-                if (!__any(have)) break;
-                continue;
-            }
-#else
             // refill the idle lanes from the queue once at least F.wf_refill of them are idle (a refill costs
             // the wave a memory round trip for the rays before their first step), or when the queue's
             // rest fits them, or when no lane traces
@@ -491,12 +418,12 @@ wave_kernel(DevScene S, FrameParams F, LaunchConst C, float* __restrict__ out, u
                 const unsigned qq = lane_prefix(idle, next);
                 if (!tracing && qq < n) {
                     myq = qq;
-                    const float4 a = wf_ld(&rb0[qq]), b = wf_ld(&rb1[qq]);
+                    const float4 a = rb0[qq], b = rb1[qq];
                     const bool sun = as_i(b.z) != 0;
                     tracing = !fast_init<COUNT>(S, T, rtm_v3(a.x, a.y, a.z), sun ? C.sun : rtm_v3(a.w, b.x, b.y), c);
                     if (WIDE) T.item = S.wroot_ref;
                     T.any = sun && F.sun_any != 0;
-                    if (!tracing) wf_st(&hb[qq], make_float2(T.bk, as_f(-1)));
+                    if (!tracing) hb[qq] = make_float2(T.bk, as_f(-1));
                 }
                 next += (unsigned)__popcll(idle);
             }
@@ -504,13 +431,12 @@ wave_kernel(DevScene S, FrameParams F, LaunchConst C, float* __restrict__ out, u
                 if (next >= n) break;
                 continue;
             }
-#endif
             if (tracing) {
-                const bool done = WIDE ? wide_step<COUNT, OVF, RT_WF_PK != 0>(T, nb, tb, lst, c)
+                const bool done = WIDE ? wide_step<COUNT, OVF>(T, nb, tb, lst, c)
                                        : fast_step<COUNT, false, OVF>(S, T, nb, tb, lst, 16u, c);
                 if (done) {
                     tracing = false;
-                    wf_st(&hb[myq], make_float2(T.bk, as_f(T.bt >= 0 ? (int)((unsigned)T.bt / 48u) : -1)));
+                    hb[myq] = make_float2(T.bk, as_f(T.bt >= 0 ? (int)((unsigned)T.bt / 48u) : -1));
                 }
             }
         }

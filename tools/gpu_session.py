@@ -19,6 +19,7 @@ STEP forms (values after '=' separated by ':'):
   kt=CFG[:OPTS]                 rocprofv3 --kernel-trace --stats of bench.py (1 step) -> gpurun_out/TAG_kt_CFG
   pmc=CFG:GROUP[:OPTS]          one rocprofv3 --pmc pass (GROUP: fetch, write, req, sq) of bench.py
   py=SCRIPT[:ARGS]              python3 -u SCRIPT ARGS (ARGS split on '+')
+  ktpy=NAME:SCRIPT[:ARGS]       rocprofv3 --kernel-trace --stats of a py step -> gpurun_out/TAG_kt_NAME
 Limits: LIMIT_<KIND> env overrides the default seconds of a step kind.
 """
 import os
@@ -30,7 +31,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 OUT = os.path.join(ROOT, "gpurun_out")
 PY = sys.executable or "python3"
 LIMITS = {"clock": 30, "pytest": 900, "bench": 300, "benchfull": 600, "smoke": 180, "ab": 600, "tiles": 400, "kt": 300,
-          "pmc": 240, "py": 600}
+          "pmc": 240, "py": 600, "ktpy": 400}
 PMC = {
     "fetch": "FETCH_SIZE",
     "write": "WRITE_SIZE",
@@ -84,6 +85,10 @@ def command(kind, val, tag, n):
             bench_args(cfg, "1", "1", opts) + ["--no-counts"], env
     if kind == "py":
         return [PY, "-u", p[0]] + (p[1].split("+") if len(p) > 1 and p[1] else []), env
+    if kind == "ktpy":
+        name = f"{tag}_kt_{p[0]}"
+        return ["rocprofv3", "--kernel-trace", "--stats", "--output-format", "csv", "-d", os.path.join(OUT, name),
+                "-o", name, "--", PY, "-u", p[1]] + (p[2].split("+") if len(p) > 2 and p[2] else []), env
     raise SystemExit(f"unknown step kind {kind!r}")
 
 

@@ -1,9 +1,10 @@
 """Summarise rocprofv3 passes of bench.py into profiles/ (committed evidence).
 
-    python tools/summarize_profiles.py gpurun_out/SESSION:CFG TAG WORKLOAD [FRAMES]
-        the kt / pmc steps of tools/gpu_session.py (gpurun_out/SESSION_kt_CFG, SESSION_pmc_CFG_GROUP)
+    python tools/summarize_profiles.py gpurun_out/SESSION:CFG[:OPTS] TAG WORKLOAD [FRAMES]
+        the kt / pmc steps of tools/gpu_session.py (gpurun_out/SESSION_kt_CFG[_OPTS],
+        SESSION_pmc_CFG_GROUP[_OPTS]; OPTS = the step's option suffix, e.g. wavefront-16)
     python tools/summarize_profiles.py DIR TAG WORKLOAD [FRAMES]
-        DIR/kt, DIR/fetch, DIR/write, DIR/req, DIR/sq (one pass each)
+        DIR/kt, DIR/fetch, DIR/write, DIR/req, DIR/sq, DIR/hit (one pass each)
 FRAMES (bench warmup + steps) is required when several render-kernel instantiations ran (two-pass
 launches), since a frame is then several dispatches.
 
@@ -36,6 +37,7 @@ import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 # FAST, uninstrumented (any variant): the megakernels and the wavefront kernel
 KERNEL = r"render(_resume)?_kernel<(0, )?false, false|wave_kernel<false"
+GROUPS = ("fetch", "write", "dram", "req", "sq", "hit")
 
 
 def _rows(pattern):
@@ -52,10 +54,11 @@ def main(prof, tag, workload, frames=None, kernel=KERNEL):
     kernel_avg_ms are then per frame (totals / frames).  Default: one dispatch per frame."""
     os.makedirs(os.path.join(ROOT, "profiles"), exist_ok=True)
     if ":" in prof:   # tools/gpu_session.py layout
-        pre, cfg = prof.split(":")
-        where = {"kt": f"{pre}_kt_{cfg}", **{g: f"{pre}_pmc_{cfg}_{g}" for g in ("fetch", "write", "dram", "req", "sq")}}
+        pre, cfg, *opt = prof.split(":")
+        sfx = "_" + opt[0] if opt and opt[0] else ""
+        where = {"kt": f"{pre}_kt_{cfg}{sfx}", **{g: f"{pre}_pmc_{cfg}_{g}{sfx}" for g in GROUPS}}
     else:
-        where = {g: os.path.join(prof, g) for g in ("kt", "fetch", "write", "dram", "req", "sq")}
+        where = {g: os.path.join(prof, g) for g in ("kt",) + GROUPS}
     stats = glob.glob(os.path.join(where["kt"], "*kernel_stats.csv"))
     if not stats:   # a run that never produced its kernel trace must not overwrite committed summaries
         sys.exit(f"no kernel trace under {where['kt']}")
@@ -78,7 +81,7 @@ def main(prof, tag, workload, frames=None, kernel=KERNEL):
             s["frames"] = int(frames) if frames else calls
             s["kernel_avg_ms"] = total / 1e6 / s["frames"]
     counters = {}
-    for sub in ("fetch", "write", "dram", "req", "sq"):
+    for sub in GROUPS:
         for r in _rows(os.path.join(where[sub], "*counter_collection.csv")):
             if re.search(kernel, r["Kernel_Name"]):
                 counters.setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))
@@ -107,6 +110,8 @@ def main(prof, tag, workload, frames=None, kernel=KERNEL):
             s["valu_lane_util"] = g("SQ_THREAD_CYCLES_VALU") / (64.0 * g("SQ_ACTIVE_INST_VALU"))
         if s.get("kernel_avg_ms"):
             s["valu_issue_frac"] = s["valu_lane_slots_per_launch"] / (s["kernel_avg_ms"] * 1e-3) / 78.6432e12
+    if g("TCC_REQ_sum"):
+        s["l2_hit_rate"] = g("TCC_HIT_sum") / max(1.0, g("TCC_HIT_sum") + g("TCC_MISS_sum"))
     with open(os.path.join(ROOT, "profiles", f"{tag}_pmc_{workload}.json"), "w") as f:
         json.dump(s, f, indent=1)
     print(json.dumps(s, indent=1))
