@@ -909,8 +909,8 @@ int rt_set_option(rt_ctx* ctx, const char* key, int64_t value) {
         return RT_OK;
     }
     if (!std::strcmp(key, "spec")) {
-        if (value != -1 && value != 0 && value != 2 && value != 4)
-            return set_err(ctx, RT_ERR_ARG, "spec must be -1 (auto), 0 (off), 2 or 4");
+        if (value != -1 && value != 0 && value != 2 && value != 4 && value != 8)
+            return set_err(ctx, RT_ERR_ARG, "spec must be -1 (auto), 0 (off), 2, 4 or 8");
         ctx->spec = (int)value;
         return RT_OK;
     }
@@ -1121,10 +1121,14 @@ hipError_t setup_pilot(rt_ctx* ctx, Device& d, rt::FrameParams& fp) {
     const int64_t lanes = (int64_t)std::max(d.cus, 1) * rt::kWalkLanesPerCu;
     // up to 4 pixels per resident lane: pass 1 finishes the pixels that draw nothing (sky), and the device
     // picks trails only when the rest is at most one pixel per lane (pilot_team_pick_kernel)
-    if (ctx->spec != 0 && fp.nloc <= 4 * lanes && !use_wide(ctx) && ctx->hs.nbrute == 0) {
+    // (auto); a set trail count applies to any tile
+    // (auto); a set trail count applies to any tile.  A trail's record count shares a word with its mode
+    // (rt_spec.hip): spp < 2^16
+    if (ctx->spec != 0 && (ctx->spec > 0 || fp.nloc <= 4 * lanes) && fp.spp < 65536 && !use_wide(ctx) &&
+        ctx->hs.nbrute == 0) {
         fp.spec = ctx->spec;   // 2 or 4 trails, or -1: chosen on the device from the pixels pass 1 left
         fp.spec_cap = fp.spp;
-        const size_t lbytes = rt::spec_log_bytes(fp);
+        const size_t lbytes = rt::spec_log_bytes(fp, d.cus);
         if (d.spec.bytes < lbytes && d.pending) e = hipEventSynchronize(d.done);
         if (e == hipSuccess) e = ensure(d.spec, lbytes);
         if (e != hipSuccess) return e;

@@ -135,7 +135,8 @@ struct FrameParams {
     uint32_t* pilot_cost;
     uint32_t* pilot_draws;   // BVH2 walk: random numbers each pixel drew in pass 1 (its RNG offset at pilot_state)
     // Pass 2 with sample-parallel speculation (rt_spec.hip, option "spec"): spec trails per pixel, each
-    // trail's log of (RNG offset, sample colour) records, spec_cap records per trail
+    // trail's log of (RNG offset, sample colour) records, spec_cap records per trail; one log per resident
+    // lane (a team's trails log the pixel it holds; the logs are reused from record 0 for its next pixel)
     int32_t spec;
     float4* spec_log;
     int32_t spec_cap;
@@ -168,14 +169,14 @@ size_t wavefront_bytes(const DevScene& sc, const FrameParams& fp, int block);
 hipError_t launch_wavefront(const DevScene& sc, const FrameParams& fp, int block, float* d_out,
                             unsigned long long* d_counts, unsigned int* d_work, hipStream_t stream);
 // Sample-parallel speculation (rt_spec.hip): pass 2 of a pilot launch of the BVH2 walk with fp.spec
-// trails per pixel; spec_log_bytes = the size of fp.spec_log it needs
-// at most kSpecTrails trails per pixel; a log holds kSpecTrails - 1 trails per pixel whatever the count;
+// trails per pixel; spec_log_bytes = the size of fp.spec_log it needs on a device of `cus` CUs (one log
+// per resident lane, launch_spec keeps the grid within them); at most kSpecTrails trails per pixel;
 // the device pick of pass 2 encodes "T trails" as kSpecPick + T in FrameParams::walk_team_dev
-constexpr int kSpecTrails = 4;
+constexpr int kSpecTrails = 8;
 constexpr int kSpecPick = 10;
 // resident lanes per CU of the BVH2 walks (render_resume_kernel, spec_kernel: 4 waves per SIMD)
 constexpr int kWalkLanesPerCu = 4 * 4 * 64;
-size_t spec_log_bytes(const FrameParams& fp);
+size_t spec_log_bytes(const FrameParams& fp, int cus);
 hipError_t launch_spec(const DevScene& sc, const FrameParams& fp, int block, float* d_out, unsigned int* d_work,
                        hipStream_t stream);
 bool spec_walk(const DevScene& sc, const FrameParams& fp);

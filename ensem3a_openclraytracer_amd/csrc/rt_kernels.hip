@@ -782,14 +782,16 @@ __global__ void pilot_team_count_kernel(const uint32_t* __restrict__ cost, int64
 }
 
 // spec: with speculation available (FrameParams::spec < 0, auto) the same thresholds pick trails instead of
-// teams: 4 trails per pixel at u <= 1/2 per lane, 2 at u <= 1 (r04, 1/8 and 1/4 row tiles: C4 1/8 u ~ 0.23
-// per lane: 4 trails 85 ms, teams 109, 2 trails 137; C3 1/8 u ~ 0.47: 2 / 4 trails 36.1 / 36.2 ms, teams
-// 50.7; C3 1/4 u ~ 0.93: 2 trails 53.8, 4 trails 61.6, teams 66.8), encoded kSpecPick + trails
+// teams: 8 trails per pixel at u <= 1/4 per lane, 4 at u <= 1/2, 2 at u <= 1 (r04, 1/8 and 1/4 row tiles:
+// C4 1/8 u ~ 0.23 per lane: 8 trails 82.1 ms, 4 trails 91.0 (85 on another box), teams 109, 2 trails 137;
+// C3 1/8 u ~ 0.47: 2 / 4 / 8 trails 36.1 / 35.0 / 41.7 ms, teams 50.7; C3 1/4 u ~ 0.93: 2 trails 53.8,
+// 4 trails 58.1-61.6, teams 66.8; whole frames (u ~ 1.8 C4, ~3.7 C3): 2 trails 302 / 151 vs one lane 300 /
+// 125 ms), encoded kSpecPick + trails
 __global__ void pilot_team_pick_kernel(const unsigned* __restrict__ left, int64_t lanes, int spec, int* __restrict__ ts) {
     if (blockIdx.x == 0 && threadIdx.x == 0) {
-        const int64_t u2 = 2 * (int64_t)*left;   // 2 u lanes
-        const int k = u2 <= lanes ? 4 : u2 <= 2 * lanes ? 2 : 1;
-        *ts = (spec && k > 1) ? kSpecPick + k : k;
+        const int64_t u4 = 4 * (int64_t)*left;   // 4 u lanes
+        const int k = u4 <= 2 * lanes ? 4 : u4 <= 4 * lanes ? 2 : 1;
+        *ts = (spec && k > 1) ? kSpecPick + (u4 <= lanes ? 8 : k) : k;
     }
 }
 

@@ -43,7 +43,7 @@ template <bool OVF, int TR>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4)))
 spec_kernel(DevScene S, FrameParams F, float* __restrict__ out, unsigned int* __restrict__ work_counter,
             const LaunchConst* __restrict__ lconst) {
-    static_assert(TR == 2 || TR == 4, "trails per pixel");
+    static_assert(TR == 2 || TR == 4 || TR == 8, "trails per pixel");
     // trails chosen on the device (pilot_team_pick_kernel): only the instantiation picked renders
     if (F.walk_team_dev && __builtin_amdgcn_readfirstlane(*F.walk_team_dev) != kSpecPick + TR) return;
     extern __shared__ int lds_stack[];
@@ -61,9 +61,12 @@ spec_kernel(DevScene S, FrameParams F, float* __restrict__ out, unsigned int* __
     const int tau = lane & (TR - 1);           // this lane's trail
     const int team0 = lane - tau;
     const bool leader = tau == 0;
-    const unsigned long long leaders = TR == 2 ? 0x5555555555555555ull : 0x1111111111111111ull;
-    auto log_at = [&](int p, int u, int k) -> float4* {   // record k of trail u (>= 1) of pixel p
-        return F.spec_log + ((size_t)p * (kSpecTrails - 1) + (size_t)(u - 1)) * (size_t)cap + (size_t)k;
+    const unsigned long long leaders = TR == 2 ? 0x5555555555555555ull : TR == 4 ? 0x1111111111111111ull : 0x0101010101010101ull;
+    // record k of trail u (>= 1) of the team's pixel: the log of the trail's lane (launch_spec: grid x block
+    // <= the logs allocated)
+    const unsigned glane0 = blockIdx.x * blockDim.x + (threadIdx.x - (unsigned)tau);
+    auto log_at = [&](int u, int k) -> float4* {
+        return F.spec_log + (size_t)(glane0 + (unsigned)u) * (size_t)cap + (size_t)k;
     };
 
     int phase = FETCH;
@@ -96,7 +99,9 @@ spec_kernel(DevScene S, FrameParams F, float* __restrict__ out, unsigned int* __
     int dcur = 0;                   // draws of the current sample so far
     int D0 = 0;                     // the pass-1 offset and words: the words at any offset >= D0 are stepped from them
     uint32_t w00 = 0, w10 = 0;
-    int cur1 = 0, cur2 = 0, cur3 = 0;   // cursors into the logs of trails tau+1.. (by trail index 1..3)
+    int cur[TR - 1];                // cursors into the logs of trails tau+1.. (trail u at [u - 1])
+#pragma unroll
+    for (int u = 0; u < TR - 1; ++u) cur[u] = 0;
     int src = 0, sj = 0;            // trail 0 stitching: the trail it follows and the next record
 
     auto restart_sample = [&]() __attribute__((always_inline)) {   // sample start from the cached camera hit / prefix
@@ -112,12 +117,12 @@ spec_kernel(DevScene S, FrameParams F, float* __restrict__ out, unsigned int* __
         phase = PREP;
     };
     // is offset x in trail u's log (u > tau)?  advances the cursor; returns the record index or -1
-    auto find_in = [&](int u, int& cur, int x, int produced) -> int {
-        while (cur < produced) {
-            const int o = (int)(__float_as_uint(log_at(p, u, cur)->x) & ~kFixedBit);
+    auto find_in = [&](int u, int& cu, int x, int produced) -> int {
+        while (cu < produced) {
+            const int o = (int)(__float_as_uint(log_at(u, cu)->x) & ~kFixedBit);
             if (o > x) return -1;
-            if (o == x) return cur;
-            ++cur;
+            if (o == x) return cu;
+            ++cu;
         }
         return -1;
     };
@@ -155,7 +160,8 @@ spec_kernel(DevScene S, FrameParams F, float* __restrict__ out, unsigned int* __
                     cd = camera_dir(C, W, i);
                     pre = false;
                     sun_c = SPEC_SUN_UNKNOWN;
-                    cur1 = cur2 = cur3 = 0;
+#pragma unroll
+                    for (int u = 0; u < TR - 1; ++u) cur[u] = 0;
                     if (s0 >= spp) {
                         phase = FETCH;   // finished in pass 1: already written
                     } else if (leader) {
@@ -184,20 +190,33 @@ spec_kernel(DevScene S, FrameParams F, float* __restrict__ out, unsigned int* __
 
         // -- the team's trails, after the hand-out (records are append-only: a count
         //    taken before this iteration's logging is a lower bound) --
-        const int prod1 = __shfl(s, team0 + 1, 64), mode1 = __shfl(mode, team0 + 1, 64), Dn1 = __shfl(D, team0 + 1, 64);
-        int prod2 = 0, mode2 = TM_IDLE, Dn2 = 0, prod3 = 0, mode3 = TM_IDLE, Dn3 = 0;
-        if (TR == 4) {
-            prod2 = __shfl(s, team0 + 2, 64); mode2 = __shfl(mode, team0 + 2, 64); Dn2 = __shfl(D, team0 + 2, 64);
-            prod3 = __shfl(s, team0 + 3, 64); mode3 = __shfl(mode, team0 + 3, 64); Dn3 = __shfl(D, team0 + 3, 64);
+        // (s | mode << 16 of every trail of the team, and its offset, by one shuffle each)
+        int sm_[TR], dn_[TR];
+#pragma unroll
+        for (int u = 1; u < TR; ++u) {
+            sm_[u] = __shfl(s | (mode << 16), team0 + u, 64);
+            dn_[u] = __shfl(D, team0 + u, 64);
         }
-        auto produced = [&](int u) { return u == 1 ? prod1 : u == 2 ? prod2 : prod3; };
-        auto mode_of = [&](int u) { return u == 1 ? mode1 : u == 2 ? mode2 : mode3; };
-        auto dnow_of = [&](int u) { return u == 1 ? Dn1 : u == 2 ? Dn2 : Dn3; };
-        auto cursor = [&](int u) -> int& { return u == 1 ? cur1 : u == 2 ? cur2 : cur3; };
-        // the first trail ahead of `from` whose log holds offset x: (trail, record) or (0, -1)
+        // trail u's value, for a runtime u (a select chain: the arrays stay in registers)
+        auto pick = [&](const int* a, int u) __attribute__((always_inline)) {
+            int v = 0;
+#pragma unroll
+            for (int w = 1; w < TR; ++w) v = u == w ? a[w] : v;
+            return v;
+        };
+        auto produced = [&](int u) { return pick(sm_, u) & 0xffff; };
+        auto mode_of = [&](int u) { return pick(sm_, u) >> 16; };
+        auto dnow_of = [&](int u) { return pick(dn_, u); };
+        // the first trail ahead of `from` whose log holds offset x: (trail, record) or (0, -1); one copy of
+        // the log scan, the cursors read and written by select chains (they stay in registers)
         auto search = [&](int from, int x, int* rec) -> int {
             for (int u = from + 1; u < TR; ++u) {
-                const int r = find_in(u, cursor(u), x, produced(u));
+                int cu = 0;
+#pragma unroll
+                for (int w = 1; w < TR; ++w) cu = u == w ? cur[w - 1] : cu;
+                const int r = find_in(u, cu, x, produced(u));
+#pragma unroll
+                for (int w = 1; w < TR; ++w) cur[w - 1] = u == w ? cu : cur[w - 1];
                 if (r >= 0) {
                     *rec = r;
                     return u;
@@ -217,7 +236,7 @@ spec_kernel(DevScene S, FrameParams F, float* __restrict__ out, unsigned int* __
                     float4 r[8];
 #pragma unroll
                     for (int k = 0; k < 8; ++k)
-                        if (k < nr) r[k] = *log_at(p, src, sj + k);
+                        if (k < nr) r[k] = *log_at(src, sj + k);
 #pragma unroll
                     for (int k = 0; k < 8; ++k) {
                         if (k < nr && mode == TM_STITCH) {
@@ -273,7 +292,7 @@ spec_kernel(DevScene S, FrameParams F, float* __restrict__ out, unsigned int* __
                         return;
                     }
                 } else {
-                    *log_at(p, tau, s) = make_float4(__uint_as_float((uint32_t)D | (fixed ? kFixedBit : 0u)), so.x,
+                    *log_at(tau, s) = make_float4(__uint_as_float((uint32_t)D | (fixed ? kFixedBit : 0u)), so.x,
                                                      so.y, so.z);
                     ++s;
                     if (fixed || s >= cap) {
@@ -413,18 +432,19 @@ const void* spec_fn() {
 
 }  // namespace
 
-size_t spec_log_bytes(const FrameParams& fp) {
+size_t spec_log_bytes(const FrameParams& fp, int cus) {
     if (fp.spec == 0) return 0;
-    return (size_t)fp.nloc * (size_t)(kSpecTrails - 1) * (size_t)std::max(fp.spp, 1) * sizeof(float4);
+    return (size_t)std::max(cus, 1) * kWalkLanesPerCu * (size_t)std::max(fp.spec_cap, 1) * sizeof(float4);
 }
 
 hipError_t launch_spec(const DevScene& sc, const FrameParams& fp, int block, float* d_out, unsigned int* d_work,
                        hipStream_t stream) {
-    if ((fp.spec != 2 && fp.spec != 4) || fp.pass != 2 || !fp.spec_log || !fp.pilot_draws || fp.spec_cap <= 0)
+    if ((fp.spec != 2 && fp.spec != 4 && fp.spec != 8) || fp.pass != 2 || !fp.spec_log || !fp.pilot_draws || fp.spec_cap <= 0)
         return hipErrorInvalidValue;
     const bool ovf = sc.stack_lds < sc.depth;
-    const void* fn = fp.spec == 2 ? (ovf ? spec_fn<true, 2>() : spec_fn<false, 2>())
-                                  : (ovf ? spec_fn<true, 4>() : spec_fn<false, 4>());
+    const void* fn = fp.spec == 2   ? (ovf ? spec_fn<true, 2>() : spec_fn<false, 2>())
+                     : fp.spec == 4 ? (ovf ? spec_fn<true, 4>() : spec_fn<false, 4>())
+                                    : (ovf ? spec_fn<true, 8>() : spec_fn<false, 8>());
     const size_t lds = (size_t)2 * std::max(sc.stack_lds, 1) * (size_t)block * sizeof(int);
     int dev = 0, cus = 0, per_cu = 0;
     hipError_t e = hipGetDevice(&dev);
@@ -432,7 +452,9 @@ hipError_t launch_spec(const DevScene& sc, const FrameParams& fp, int block, flo
     if (e == hipSuccess) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, block, lds);
     if (e != hipSuccess) return e;
     const int cap_cu = fp.max_waves > 0 ? std::max(1, fp.max_waves * 4 * 64 / block) : INT_MAX;
-    const int64_t resident = (int64_t)std::max(1, cus) * std::max(1, std::min(per_cu, cap_cu));
+    // at most kWalkLanesPerCu lanes per CU: one trail log each (spec_log_bytes)
+    const int cap_logs = std::max(1, kWalkLanesPerCu / block);
+    const int64_t resident = (int64_t)std::max(1, cus) * std::max(1, std::min({per_cu, cap_cu, cap_logs}));
     const int64_t grid = std::min<int64_t>((fp.nloc * fp.spec + block - 1) / block, resident);
     // the work block's counters and launch constants were set up by pass 1's launch (launch_t): pass 2
     // re-zeroes the counters and recomputes the constants the same way

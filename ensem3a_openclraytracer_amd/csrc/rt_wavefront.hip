@@ -52,12 +52,13 @@ enum WfPlane {
 constexpr int wf_planes(bool prefix) { return prefix ? (int)WF_ALL : (int)WF_CORE; }
 // per queue entry besides the planes: ray (o.xyz d.x | d.yz flags -) 32 B + hit (k, triangle) 8 B
 constexpr int kWfEntryBytes = 40;
-// LDS stack entries per lane: 8 waves per SIMD x 4 SIMDs x 64 lanes x 10 x 8 B = 160 KB, the CU's LDS
-constexpr int kStackLdsWave = 10;
 #ifndef RT_WF_WAVES
 #define RT_WF_WAVES 8
 #endif
 constexpr int kWfWaves = RT_WF_WAVES;
+// LDS stack entries per lane: the CU's 160 KB over its lanes (8 waves per SIMD x 4 SIMDs x 64 lanes x 10 x
+// 8 B; 20 entries at 4 waves)
+constexpr int kStackLdsWave = 80 / kWfWaves;
 constexpr int SUN_UNKNOWN = -2;
 // dirty bits: state rows rewritten in place only where they changed
 constexpr unsigned D_P = 1, D_SEED = 2, D_SM = 4, D_KCTC = 8, D_SUNC = 16;

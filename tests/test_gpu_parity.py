@@ -1084,7 +1084,7 @@ def test_speculative_trails_render_identically(kl, case):
     kl.native.set_option("bvh_width", 2)
     try:
         frames = {}
-        for trails in (0, 2, 4):
+        for trails in (0, 2, 4, 8):
             kl.native.set_option("spec", trails)
             for pilot in (2, 5):
                 kl.native.set_option("pilot", pilot)
@@ -1103,7 +1103,7 @@ def test_speculative_trails_render_identically(kl, case):
 @pytest.mark.parametrize("config,row0,step", [("C3", 3, 8), ("C4", 5, 8)])
 def test_speculative_trails_row_tiles(kl, config, row0, step):
     """A 1/8 row tile of the full-size C3 / C4 frame (the multi-GPU regime) at 64 spp with the automatic
-    small-tile pilot: 2 and 4 trails per pixel give the one-lane tile bit for bit."""
+    small-tile pilot: 2, 4 and 8 trails per pixel give the one-lane tile bit for bit."""
     import torch
     from ensem3a_openclraytracer_amd import distributed as D
     sc, cam, env, npix, _, mb, ibl = W.CONFIGS[config].inputs()
@@ -1114,7 +1114,7 @@ def test_speculative_trails_row_tiles(kl, config, row0, step):
     out = torch.empty(3 * width * D.tile_rows(npix, width, row0, step), dtype=torch.float32, device="cuda")
     frames = []
     try:
-        for trails in (0, 2, 4):
+        for trails in (0, 2, 4, 8):
             ctx.set_option("spec", trails)
             ctx.render_device(cam, env, npix, spp, mb, row0, step, out.data_ptr())
             torch.cuda.synchronize()

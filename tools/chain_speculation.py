@@ -115,7 +115,7 @@ def main():
     mus = np.array([chain(nd, spp + 1)[-1] / spp for _, _, nd, _ in tr])
     print(f"{name}: {npx} pixels, draws/sample mean {mus.mean():.2f} (std {mus.std():.2f}); serial chain "
           f"mean {ser.mean():.1f} rays, max {ser.max()}")
-    for T in (2, 3, 4):
+    for T in [int(x) for x in os.environ.get("SPEC_TRAILS", "2,3,4").split(",")]:
         r = [speculate(nd, nr, spp, T, mu if mu > 0 else pilot_mu(nd, spp, max(spp // 8, 1)))
              for _, _, nd, nr in tr]
         lat = np.array([a for a, _ in r], float)

@@ -5,6 +5,9 @@
         SESSION_pmc_CFG_GROUP[_OPTS]; OPTS = the step's option suffix, e.g. wavefront-16)
     python tools/summarize_profiles.py DIR TAG WORKLOAD [FRAMES]
         DIR/kt, DIR/fetch, DIR/write, DIR/req, DIR/sq, DIR/hit (one pass each)
+    --wave-stats FILE:CONFIG  also record the SIMD efficiency of the render loop (tools/wave_stats.py's
+        JSON line for CONFIG in FILE: trav_simd_eff = items advanced per lane-step of the traversal, beside
+        valu_lane_util, which the predicated steps inflate)
 FRAMES (bench warmup + steps) is required when several render-kernel instantiations ran (two-pass
 launches), since a frame is then several dispatches.
 
@@ -48,7 +51,7 @@ def _rows(pattern):
     return out
 
 
-def main(prof, tag, workload, frames=None, kernel=KERNEL):
+def main(prof, tag, workload, frames=None, kernel=KERNEL, wave_stats=None):
     """frames: frames the profiled run rendered (bench warmup + steps).  A frame may take several
     dispatches of the render kernel (two-pass launches, option "pilot"); every *_per_launch value and
     kernel_avg_ms are then per frame (totals / frames).  Default: one dispatch per frame."""
@@ -110,6 +113,14 @@ def main(prof, tag, workload, frames=None, kernel=KERNEL):
             s["valu_lane_util"] = g("SQ_THREAD_CYCLES_VALU") / (64.0 * g("SQ_ACTIVE_INST_VALU"))
         if s.get("kernel_avg_ms"):
             s["valu_issue_frac"] = s["valu_lane_slots_per_launch"] / (s["kernel_avg_ms"] * 1e-3) / 78.6432e12
+    if wave_stats:
+        path, cfg = wave_stats.rsplit(":", 1)
+        with open(path) as f:
+            rows = [json.loads(ln) for ln in f if ln.strip()]
+        row = [r for r in rows if r["config"] == cfg and not r.get("opts")][-1]
+        for k in ("trav_simd_eff", "trav_iters_per_wave_render_iter", "rays_per_lane_render_iter", "trav_cycle_share"):
+            s[k] = row[k]
+        s["wave_stats_note"] = "tools/wave_stats.py (instrumented kernel, product defaults): " + os.path.basename(path)
     if g("TCC_REQ_sum"):
         s["l2_hit_rate"] = g("TCC_HIT_sum") / max(1.0, g("TCC_HIT_sum") + g("TCC_MISS_sum"))
     with open(os.path.join(ROOT, "profiles", f"{tag}_pmc_{workload}.json"), "w") as f:
@@ -118,4 +129,10 @@ def main(prof, tag, workload, frames=None, kernel=KERNEL):
 
 
 if __name__ == "__main__":
-    main(*sys.argv[1:5])
+    args = sys.argv[1:]
+    ws = None
+    if "--wave-stats" in args:
+        i = args.index("--wave-stats")
+        ws = args[i + 1]
+        del args[i:i + 2]
+    main(*args[:4], wave_stats=ws)
