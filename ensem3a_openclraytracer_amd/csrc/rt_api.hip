@@ -1087,15 +1087,11 @@ hipError_t setup_pilot(rt_ctx* ctx, Device& d, rt::FrameParams& fp) {
         // when they are reordered: r03 row tiles 1/2, 1/4, 1/8: 3,005 / 1,626 / 937 ms without the pilot,
         // 3,185 / 1,694 / 938 with it
         if (ctx->hs.nbrute > 0 || use_wide(ctx) || fp.spp < 16 || fp.nloc > 16 * lanes) return hipSuccess;
-        if (fp.nloc <= lanes) {
-            // small tiles (multi-GPU row tiles) of the BVH2 walk, whose pixels get teams of lanes
-            // (walk_team): the cost order starts the long chains first, pilot spp/16 (r03, 1/8 tiles:
-            // C3 62.6 -> 49.3 ms, C4 168 -> 142 ms; spp/8: 49.9 / 145.9)
-            if (fp.spp < 32) return hipSuccess;
-            k = fp.spp / 16;
-        } else {
-            k = fp.spp / 8;
-        }
+        // spp/8 samples, small tiles (multi-GPU row tiles, whose pass 2 takes teams or speculative trails)
+        // included: r04 1/8 tiles with trails, pilot spp/16 / spp/8 / 3spp/16: C4 80.8 / 78.3 / 77.0 ms,
+        // C3 35.3 / 33.9 / 35.1 ms; 1/4 tiles C4 120.7 / 119.9 / 129.1, C3 54.8 / 54.8 / 56.1 (r03, teams
+        // without trails, had preferred spp/16: C3 49.3 vs 49.9, C4 142 vs 146)
+        k = fp.spp / 8;
     }
     if (k >= fp.spp) return hipSuccess;
     const size_t n = (size_t)fp.nloc;
