@@ -621,6 +621,10 @@ hipError_t upload(DevBuf& b, const std::vector<T>& v, hipStream_t s) {
     return hipMemcpyAsync(b.p, v.data(), bytes, hipMemcpyHostToDevice, s);
 }
 
+int effective_traversal(const rt_ctx* ctx) {
+    return (ctx->traversal == RT_TRAVERSAL_FAST && ctx->hs.fast_ok) ? RT_TRAVERSAL_FAST : RT_TRAVERSAL_REF;
+}
+
 // The 4-wide layout serves the walk when chosen, or (auto) when the BVH2 node array exceeds
 // rt::kWideMinBytes.
 bool use_wide(const rt_ctx* ctx) {
@@ -713,7 +717,10 @@ int check_frame(rt_ctx* ctx, const float* cam, const float* env, int64_t npix, i
     fp->team = ctx->team;
     fp->walk_team = ctx->walk_team;
     fp->max_waves = ctx->max_waves;
-    fp->handout = ctx->handout > 0 ? 1 : 0;
+    // auto: contiguous per-XCD blocks on the 4-wide walk (C5, same-box A/B twice: 4,998 / 4,984 -> 4,952 /
+    // 4,958 ms per frame; its L2-missing walk keeps neighbouring pixels on one XCD's L2), interleaved chunks
+    // elsewhere (C3 / C4 -0.5 / +1 %, brute force untested)
+    fp->handout = ctx->handout >= 0 ? ctx->handout : (use_wide(ctx) && effective_traversal(ctx) == RT_TRAVERSAL_FAST);
     fp->wf_slots = ctx->wavefront > 0 ? ctx->wavefront : (ctx->wavefront < 0 ? auto_wavefront(ctx, *fp) : 0);
     fp->wf_buf = nullptr;
     fp->wf_refill = ctx->wf_refill > 0 ? ctx->wf_refill : kWfRefillAuto;
@@ -721,10 +728,6 @@ int check_frame(rt_ctx* ctx, const float* cam, const float* env, int64_t npix, i
     fp->log_cap = 0;
     fp->log_count = nullptr;
     return RT_OK;
-}
-
-int effective_traversal(const rt_ctx* ctx) {
-    return (ctx->traversal == RT_TRAVERSAL_FAST && ctx->hs.fast_ok) ? RT_TRAVERSAL_FAST : RT_TRAVERSAL_REF;
 }
 
 }  // namespace
