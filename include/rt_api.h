@@ -85,11 +85,19 @@ int rt_set_env(rt_ctx* ctx, const uint8_t* rgba, int w, int h);
  * size), "walk_team" (BVH2 tree walk: 1/2/4/8 lanes walk each ray of a pixel
  * together, 0 = auto: 4 on tiles of at most one pixel per resident lane and
  * on the second pass of a pilot launch from the pixels its first pass left --
- * same hits), "waves" (persistent grid: at most this many waves per SIMD, 0 =
- * occupancy limit), "block" (threads per block: 64, 128 or 256), and the
- * tuning switches documented in DESIGN.md 4.2 ("sun_skip", "sun_any",
- * "fixed_point", "sun_cache", "pilot", "pilot_chunk", "pilot_levels", "stack_lds",
- * "bvh_width"): every option renders the same frame.
+ * same hits), "spec" (second pass of a pilot launch of the BVH2 walk: 2/4/8
+ * speculative trails per pixel from guessed RNG offsets, stitched in chain
+ * order, 0 = off, -1 = auto: chosen on the device on small tiles -- same
+ * frame), "wavefront" (tree walk split into trace / shade phases per wave with
+ * K path slots per lane in HBM, 0 = the per-lane kernel, -1 = auto = 0 --
+ * same frame), "handout" (1 = a contiguous pixel block per XCD group, 0 =
+ * interleaved chunks, -1 = auto: 1 on the 4-wide walk), "waves" (persistent
+ * grid: at most this many waves per SIMD, 0 = occupancy limit), "block"
+ * (threads per block: 64, 128 or 256), and the tuning switches documented in
+ * DESIGN.md 4.2 ("sun_skip", "sun_any", "fixed_point", "sun_cache", "pilot",
+ * "pilot_chunk", "pilot_levels", "stack_lds", "ref_stack", "wf_refill",
+ * "bvh_width"): every option renders the same frame except "ref_stack" (REF's
+ * stack slots; 20 = the reference's, more = no silent drops).
  * "bvh" and "brute_max" may be changed after rt_set_scene. */
 int rt_set_option(rt_ctx* ctx, const char* key, int64_t value);
 
