@@ -16,8 +16,9 @@ STEP forms (values after '=' separated by ':'):
   smoke                         __graft_entry__.smoke()
   ab=CFGS:SPECS                 tools/ab_walk.py SPECS with AB_CFGS=CFGS (SPECS = name[@k=v+k=v]:block,...)
   tiles=CFG:NS[:SETS]           tools/occupancy_probe.py CFG NS "SETS" (SETS: k=v,k=v;k=v)
-  kt=CFG[:OPTS]                 rocprofv3 --kernel-trace --stats of bench.py (1 step) -> gpurun_out/TAG_kt_CFG
-  pmc=CFG:GROUP[:OPTS]          one rocprofv3 --pmc pass (GROUP: fetch, write, req, sq) of bench.py
+  kt=CFG[:OPTS[:STEPS]]         rocprofv3 --kernel-trace --stats of bench.py (STEPS steps, default 1, after 1
+                                warmup) -> gpurun_out/TAG_kt_CFG
+  pmc=CFG:GROUP[:OPTS[:STEPS]]  one rocprofv3 --pmc pass (GROUP: fetch, write, req, sq, hit) of bench.py
   py=SCRIPT[:ARGS]              python3 -u SCRIPT ARGS (ARGS split on '+')
   ktpy=NAME:SCRIPT[:ARGS]       rocprofv3 --kernel-trace --stats of a py step -> gpurun_out/TAG_kt_NAME
 Limits: LIMIT_<KIND> env overrides the default seconds of a step kind.
@@ -78,11 +79,12 @@ def command(kind, val, tag, n):
     if kind in ("kt", "pmc"):
         cfg = p[0]
         opts = (p[2] if len(p) > 2 else "") if kind == "pmc" else (p[1] if len(p) > 1 else "")
+        nst = (p[3] if len(p) > 3 else "1") if kind == "pmc" else (p[2] if len(p) > 2 else "1")
         name = f"{tag}_{kind}_{cfg}" + (f"_{p[1]}" if kind == "pmc" else "") + \
             ("_" + "".join(ch if ch.isalnum() else "-" for ch in opts) if opts else "")
         prof = ["rocprofv3"] + (["--kernel-trace", "--stats"] if kind == "kt" else ["--pmc"] + PMC[p[1]].split())
         return prof + ["--output-format", "csv", "-d", os.path.join(OUT, name), "-o", name, "--"] + \
-            bench_args(cfg, "1", "1", opts) + ["--no-counts"], env
+            bench_args(cfg, nst or "1", "1", opts) + ["--no-counts"], env
     if kind == "py":
         return [PY, "-u", p[0]] + (p[1].split("+") if len(p) > 1 and p[1] else []), env
     if kind == "ktpy":
