@@ -50,7 +50,7 @@ struct Device {
     hipStream_t stream = nullptr;
     int cus = 0;                  // compute units (sizes the FAST stack overflow buffer)
     DevBuf stack_ovf;             // FAST traversal stack entries beyond the LDS part
-    DevBuf nodes, wnodes, wleaves, tri_fast, brute, brute_box, bvh9, tri_geo, tri_shade, tri_frame, mat, ibl, out, out8, counts, work, scratch_a, scratch_b;
+    DevBuf nodes, wnodes, wleaves, tri_fast, brute, brute_box, bvh9, tri_geo, tri_shade, tri_frame, mat, ibl, ibl_sum, out, out8, counts, work, scratch_a, scratch_b;
     DevBuf pilot;                 // two-pass launches: per-pixel state, cost and order (FrameParams::pilot_*)
     DevBuf wf;                    // wavefront launches: the waves' path-state regions (FrameParams::wf_buf)
     DevBuf spec;                  // speculation: the trails' sample logs (FrameParams::spec_log)
@@ -652,7 +652,7 @@ rt::DevScene dev_scene(const rt_ctx* ctx, const Device& d) {
     s.ntri = ctx->hs.ntri;
     s.mat = (const float*)d.mat.p;
     s.nmat = ctx->hs.nmat;
-    s.ibl = (const uchar4*)d.ibl.p;
+    s.ibl_sum = (const uint32_t*)d.ibl_sum.p;
     s.ibl_w = ctx->ibl_w;
     s.ibl_h = ctx->ibl_h;
     // stack sized for whichever layout the launch picks (launch_fast uses the wide one only for the
@@ -777,7 +777,7 @@ void rt_destroy(rt_ctx* ctx) {
         if (hipSetDevice(d.id) != hipSuccess) continue;
         if (d.pending) (void)hipEventSynchronize(d.done);
         if (d.stream) (void)hipStreamSynchronize(d.stream);
-        for (DevBuf* b : {&d.stack_ovf, &d.nodes, &d.wnodes, &d.wleaves, &d.tri_fast, &d.brute, &d.brute_box, &d.bvh9, &d.tri_geo, &d.tri_shade, &d.tri_frame, &d.mat, &d.ibl, &d.out,
+        for (DevBuf* b : {&d.stack_ovf, &d.nodes, &d.wnodes, &d.wleaves, &d.tri_fast, &d.brute, &d.brute_box, &d.bvh9, &d.tri_geo, &d.tri_shade, &d.tri_frame, &d.mat, &d.ibl, &d.ibl_sum, &d.out,
                           &d.out8, &d.counts, &d.work, &d.scratch_a, &d.scratch_b, &d.pilot, &d.wf, &d.spec})
             release(*b);
         if (d.host_stage) (void)hipHostFree(d.host_stage);
@@ -1060,7 +1060,9 @@ int rt_set_env(rt_ctx* ctx, const uint8_t* rgba, int w, int h) {
         HIP_OR_RET(ctx, order_after_last(d, d.stream));
         HIP_OR_RET(ctx, hipStreamSynchronize(d.stream));   // the old IBL buffer may be freed by ensure
         HIP_OR_RET(ctx, ensure(d.ibl, bytes));
+        HIP_OR_RET(ctx, ensure(d.ibl_sum, (size_t)(w + 1) * (size_t)(h + 1) * sizeof(uint32_t)));
         HIP_OR_RET(ctx, hipMemcpyAsync(d.ibl.p, rgba, bytes, hipMemcpyHostToDevice, d.stream));
+        HIP_OR_RET(ctx, rt::launch_ibl_sum((const uchar4*)d.ibl.p, w, h, (uint32_t*)d.ibl_sum.p, d.stream));
         HIP_OR_RET(ctx, hipStreamSynchronize(d.stream));
     }
     ctx->ibl_w = w;

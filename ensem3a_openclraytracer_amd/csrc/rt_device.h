@@ -594,6 +594,23 @@ __device__ __forceinline__ rtm_f3 camera_dir(const LaunchConst& C, int W, int i)
 }
 
 // ---- IBL, MathLib.cl:72-90 (integer coords through a linear sampler) ----
+// The 2x2 texel sums, per clamped coordinate (X, Y) of sample_ibl: X = 0 -> texels (0, 0); 0 < X < W -> (X - 1, X);
+// X = W -> (W - 1, W - 1) (and likewise Y), exactly the clamps of the lookup below
+__global__ void ibl_sum_kernel(const uchar4* __restrict__ rgba, int w, int h, uint32_t* __restrict__ sum) {
+    const int64_t n = (int64_t)(w + 1) * (h + 1);
+    for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < n; q += (int64_t)gridDim.x * blockDim.x) {
+        const int X = (int)(q % (w + 1)), Y = (int)(q / (w + 1));
+        const int x0 = max(min(X - 1, w - 1), 0), x1 = min(X, w - 1);
+        const int y0 = max(min(Y - 1, h - 1), 0), y1 = min(Y, h - 1);
+        const uchar4 t00 = rgba[(int64_t)y0 * w + x0], t10 = rgba[(int64_t)y0 * w + x1];
+        const uchar4 t01 = rgba[(int64_t)y1 * w + x0], t11 = rgba[(int64_t)y1 * w + x1];
+        const uint32_t r = (uint32_t)t00.x + t10.x + t01.x + t11.x;
+        const uint32_t g = (uint32_t)t00.y + t10.y + t01.y + t11.y;
+        const uint32_t b = (uint32_t)t00.z + t10.z + t01.z + t11.z;
+        sum[q] = r | (g << 10) | (b << 20);
+    }
+}
+
 template <bool COUNT>
 __device__ rtm_f3 sample_ibl(const DevScene& S, const LaunchConst& C, rtm_f3 dir, Cnt& c) {
     if (COUNT) c.env++;
@@ -607,15 +624,14 @@ __device__ rtm_f3 sample_ibl(const DevScene& S, const LaunchConst& C, rtm_f3 dir
     const int W = S.ibl_w, H = S.ibl_h;
     const int x = rtm_f2i(u * (float)W);
     const int y = rtm_f2i(v * (float)H);
-    const int x0 = min(max(x > -2147483647 ? x - 1 : x, 0), W - 1), x1 = min(max(x, 0), W - 1);
-    const int y0 = min(max(y > -2147483647 ? y - 1 : y, 0), H - 1), y1 = min(max(y, 0), H - 1);
-    const uchar4 t00 = S.ibl[(int64_t)y0 * W + x0];
-    const uchar4 t10 = S.ibl[(int64_t)y0 * W + x1];
-    const uchar4 t01 = S.ibl[(int64_t)y1 * W + x0];
-    const uchar4 t11 = S.ibl[(int64_t)y1 * W + x1];
-    const float sr = (float)((int)t00.x + (int)t10.x + (int)t01.x + (int)t11.x);
-    const float sg = (float)((int)t00.y + (int)t10.y + (int)t01.y + (int)t11.y);
-    const float sb = (float)((int)t00.z + (int)t10.z + (int)t01.z + (int)t11.z);
+    // the texels (x0, y0) .. (x1, y1) = (clamp(x - 1), clamp(y - 1)) .. (clamp(x), clamp(y)) depend on x and y
+    // only through X = clamp(x, 0, W), Y = clamp(y, 0, H): their integer channel sums are one precomputed
+    // word (ibl_sum_kernel), so a lookup is one 4-byte load instead of four texels from two rows
+    const int X = min(max(x, 0), W), Y = min(max(y, 0), H);
+    const uint32_t s4 = S.ibl_sum[(int64_t)Y * (W + 1) + X];
+    const float sr = (float)(int)(s4 & 1023u);
+    const float sg = (float)(int)((s4 >> 10) & 1023u);
+    const float sb = (float)(int)(s4 >> 20);
     const float w = 1.0f / 1020.0f;
     return rtm_scale(rtm_v3(sr * w, sg * w, sb * w), 1.0f);
 }

@@ -73,8 +73,9 @@ struct DevScene {
     // materials: the reference's 6 floats [type, r, g, b, roughness, ior] padded to kMatF = 8 (two float4)
     const float* mat;
     int32_t nmat;
-    // IBL RGBA8
-    const uchar4* ibl;
+    // IBL: the 2x2 texel sums the reference's lookup averages (ibl_sum_kernel), one word per clamped
+    // integer coordinate (X, Y) in [0, ibl_w] x [0, ibl_h]: r | g << 10 | b << 20 (each <= 4 x 255)
+    const uint32_t* ibl_sum;
     int32_t ibl_w, ibl_h;
     int32_t depth;         // max number of FAST stack entries a ray can need
     // FAST traversal stack: the first stack_lds entries of each lane in LDS, deeper ones
@@ -160,6 +161,8 @@ struct FrameParams {
 hipError_t launch_render(const DevScene& sc, const FrameParams& fp, int traversal, int block,
                          float* d_out, unsigned long long* d_counts, unsigned int* d_work, hipStream_t stream);
 hipError_t launch_prep_frames(const DevScene& sc, float4* frame, hipStream_t stream);
+// the IBL's 2x2 texel-sum table (DevScene::ibl_sum) from the RGBA8 image: (w + 1) x (h + 1) words
+hipError_t launch_ibl_sum(const uchar4* rgba, int w, int h, uint32_t* sum, hipStream_t stream);
 hipError_t launch_gamma(const float* d_in, float* d_out, int64_t n, hipStream_t stream);
 hipError_t launch_rgb8(const float* d_in, uint8_t* d_out, int64_t n, bool gamma, hipStream_t stream);
 // Wavefront tree walk (rt_wavefront.hip): whether a launch takes it, the bytes of fp.wf_buf it needs,

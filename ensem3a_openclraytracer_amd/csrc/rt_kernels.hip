@@ -971,6 +971,13 @@ hipError_t launch_debug_log(const DevScene& sc, const FrameParams& fp, int trave
     return launch_t<TRAV_FAST, false, true>(sc, fp, 64, d_out, nullptr, d_work, stream);
 }
 
+hipError_t launch_ibl_sum(const uchar4* rgba, int w, int h, uint32_t* sum, hipStream_t stream) {
+    const int64_t n = (int64_t)(w + 1) * (h + 1);
+    const unsigned grid = (unsigned)std::min<int64_t>((n + 255) / 256, 65536);
+    hipLaunchKernelGGL(ibl_sum_kernel, dim3(grid), dim3(256), 0, stream, rgba, w, h, sum);
+    return hipGetLastError();
+}
+
 hipError_t launch_prep_frames(const DevScene& sc, float4* frame, hipStream_t stream) {
     if (sc.ntri <= 0) return hipSuccess;
     hipLaunchKernelGGL(prep_frames_kernel, dim3((unsigned)((sc.ntri + 255) / 256)), dim3(256), 0, stream, sc.tri_shade,

@@ -519,6 +519,19 @@ def test_edge_cases_match_oracle(kl):
         np.testing.assert_array_equal(out, _oracle(sc, cam, env, npix, 3, 2, tiny)[: 3 * npix])
 
 
+@pytest.mark.parametrize("wh", [(1, 1), (2, 1), (3, 2), (7, 5)])
+def test_tiny_ibl_clamps_match_oracle(kl, wh):
+    """The IBL lookup reads the 2x2 texel sum of its clamped integer coordinates from a precomputed
+    table (ibl_sum_kernel).  Tiny images put most lookups on the clamped edges (x <= 0 -> texels 0, 0;
+    x >= W -> W-1, W-1); frames stay the oracle's, which averages the four texels itself."""
+    w, h = wh
+    sc, cam, env, npix, spp, mb, _ = W.PARITY_CASES["serre_96x54_s4"].inputs()
+    ibl = np.random.default_rng(w * 31 + h).integers(0, 256, (h, w, 4), dtype=np.uint8)
+    want = _oracle(sc, cam, env, npix, spp, mb, ibl)
+    np.testing.assert_array_equal(_launch(kl, sc, cam, env, npix, spp, mb, ibl, "fast"), want)
+    np.testing.assert_array_equal(_launch(kl, sc, cam, env, npix, spp, mb, ibl, "ref"), want)
+
+
 def test_empty_scene_sees_only_the_environment(kl):
     ibl = W.ibl_preview()
     cam = np.array([0, 0, 0, 0, 0, 0, 16, 16, 1, 0.785], np.float32)
