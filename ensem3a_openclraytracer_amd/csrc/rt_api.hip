@@ -116,7 +116,7 @@ struct rt_ctx {
     int wavefront = -1;   // tree walk split into trace / shade phases: path slots per lane (0 = off, -1 = auto)
     int ref_stack = 20;   // REF traversal stack capacity (20 = the reference's, stack.cl:4)
     int wf_refill = 0;    // wavefront trace phase: idle lanes that trigger a refill (0 = auto)
-    int spec = -1;        // small tiles: speculative trails per pixel in pass 2 (0 = off, 2 or 4, -1 = auto)
+    int spec = -1;        // small tiles: speculative trails per pixel in pass 2 (0 = off, 2, 4 or 8, -1 = auto)
     int handout = -1;     // pixel hand-out: 0 = interleaved chunks, 1 = a contiguous block per XCD group, -1 = auto
     std::string err;
 };
@@ -1127,7 +1127,7 @@ hipError_t setup_pilot(rt_ctx* ctx, Device& d, rt::FrameParams& fp) {
     // (rt_spec.hip): spp < 2^16
     if (ctx->spec != 0 && (ctx->spec > 0 || fp.nloc <= 4 * lanes) && fp.spp < 65536 && !use_wide(ctx) &&
         ctx->hs.nbrute == 0) {
-        fp.spec = ctx->spec;   // 2 or 4 trails, or -1: chosen on the device from the pixels pass 1 left
+        fp.spec = ctx->spec;   // 2, 4 or 8 trails, or -1: chosen on the device from the pixels pass 1 left
         fp.spec_cap = fp.spp;
         const size_t lbytes = rt::spec_log_bytes(fp, d.cus);
         if (d.spec.bytes < lbytes && d.pending) e = hipEventSynchronize(d.done);

@@ -882,7 +882,7 @@ hipError_t launch_t(const DevScene& sc, const FrameParams& fp, int block, float*
     LaunchConst* lc = reinterpret_cast<LaunchConst*>(reinterpret_cast<char*>(d_work) + kConstOffset);
     hipLaunchKernelGGL(make_const_kernel, dim3(1), dim3(64), 0, stream, f, lc);
     if (kTeamable && dev_team) {
-        // the device picks 1, 2 or 4 (pilot_team_pick_kernel): all three are launched in order, and the
+        // the device picks 1, 2 or 4 lanes (pilot_team_pick_kernel): all three are launched in order, and the
         // two whose size was not picked return at once
         int64_t g2 = 0, g4 = 0;
         e = team_grid(2, &g2);

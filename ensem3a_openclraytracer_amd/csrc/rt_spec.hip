@@ -1,5 +1,6 @@
 // Sample-parallel speculation for small tiles (option "spec"): pass 2 of a pilot launch of the BVH2
-// tree walk, when a tile has about one pixel per resident lane (the row tiles of an N-GPU frame).
+// tree walk, when a tile has about one pixel per resident lane (the row tiles of an N-GPU frame), with
+// TR = 2, 4 or 8 trails per pixel (chosen on the device, pilot_team_pick_kernel).
 //
 // A pixel's samples are one chain (Raytracing.cl:191-209): sample k starts with the RNG words after
 // D_k draws from the pixel seed (Raytracing.cl:171-172, MathLib.cl:294-310) and its colour and draw
@@ -9,7 +10,8 @@
 //   trail 0 continues the chain from the pass-1 state (offset D0 = pilot_draws, sample s0);
 //   trail t > 0 starts at a guessed offset G_t = D0 + t (spp - s0) / TR * mu, mu = D0 / s0 the pixel's
 //   draws per pilot sample, with the RNG words stepped there, and logs every sample it completes as
-//   (offset, colour) in its own log (spec_log).
+//   (offset, colour) in its own log (spec_log: one per resident lane, reused from record 0 for the
+//   team's next pixel).
 // At every sample start a trail looks its offset up in the logs of the trails ahead of it (a cursor per
 // log: offsets only grow).  Trails meet wherever one lands on an offset another computed: from there
 // on their samples coincide.  A trail t > 0 that meets stops; trail 0 that meets becomes the stitcher:
