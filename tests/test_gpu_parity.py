@@ -1113,7 +1113,7 @@ def test_speculative_trails_render_identically(kl, case):
         kl.native.set_option("spec", 3)
 
 
-@pytest.mark.parametrize("config,row0,step", [("C3", 3, 8), ("C4", 5, 8)])
+@pytest.mark.parametrize("config,row0,step", [("C3", 3, 8), ("C4", 5, 8), ("C3", 2, 5), ("C4", 0, 3)])
 def test_speculative_trails_row_tiles(kl, config, row0, step):
     """A 1/8 row tile of the full-size C3 / C4 frame (the multi-GPU regime) at 64 spp with the automatic
     small-tile pilot: 2, 4 and 8 trails per pixel give the one-lane tile bit for bit."""
