@@ -1189,7 +1189,10 @@ __device__ __forceinline__ int wide_node(float4 g0, float4 g1, float4 g2, float4
         t[a] = sw ? tb : ta; t[b] = sw ? ta : tb;
         r[a] = sw ? rb : ra; r[b] = sw ? ra : rb;
     };
-    ce(0, 1); ce(2, 3); ce(0, 2); ce(1, 3); ce(1, 2);
+    // the nearest child first (continued), the other three pushed in tournament order, not fully sorted:
+    // the order only steers the walk (r04, VALU-bound: C5 4,764 / 4,762 -> 4,726 / 4,730 ms with 2 of the
+    // 5 compare-exchanges dropped; r03, before the walk was issue-bound, it was -0.2 %)
+    ce(0, 1); ce(2, 3); ce(0, 2);
 #pragma unroll
     for (int i = 3; i >= 1; --i) {
         if (t[i] < INFINITY) {
