@@ -748,8 +748,11 @@ int rt_create(int n_devices, const int* device_ids, rt_ctx** out) {
     if (e != hipSuccess || avail <= 0)
         return set_err(nullptr, RT_ERR_HIP, "no HIP device available (%s)", hipGetErrorString(e));
     if (n_devices <= 0) n_devices = 1;
-    if (n_devices > avail)
+    // explicit ids may repeat one GPU (KernelLauncher(device=[0, 0]): two row-interleaved slots, each
+    // with its own stream and buffers); without ids the first n_devices GPUs must exist
+    if (!device_ids && n_devices > avail)
         return set_err(nullptr, RT_ERR_ARG, "requested %d devices, %d available", n_devices, avail);
+    if (n_devices > 64) return set_err(nullptr, RT_ERR_ARG, "at most 64 device slots, got %d", n_devices);
     rt_ctx* ctx = new rt_ctx();
     ctx->devs.resize(n_devices);
     for (int i = 0; i < n_devices; ++i) {
@@ -1128,11 +1131,22 @@ hipError_t setup_pilot(rt_ctx* ctx, Device& d, rt::FrameParams& fp) {
     if (ctx->spec != 0 && (ctx->spec > 0 || fp.nloc <= 4 * lanes) && fp.spp < 65536 && !use_wide(ctx) &&
         ctx->hs.nbrute == 0) {
         fp.spec = ctx->spec;   // 2, 4 or 8 trails, or -1: chosen on the device from the pixels pass 1 left
-        fp.spec_cap = fp.spp;
+        // records per trail: a trail t >= 1 starts t (spp - k) / T samples ahead, so it never needs more than
+        // spp - k records; past kSpecCapMax it stops and the chain goes on in a trail further ahead or in
+        // trail 0 (rt_spec.hip) -- the frame does not depend on the cap, the log size (CUs x lanes x cap x
+        // 16 B, at most 1 GB on 256 CUs) no longer grows with spp
+        fp.spec_cap = std::min(fp.spp - k, rt::kSpecCapMax);
         const size_t lbytes = rt::spec_log_bytes(fp, d.cus);
         if (d.spec.bytes < lbytes && d.pending) e = hipEventSynchronize(d.done);
         if (e == hipSuccess) e = ensure(d.spec, lbytes);
-        if (e != hipSuccess) return e;
+        if (e != hipSuccess) {
+            if (ctx->spec > 0) return e;
+            // auto: a device short of memory renders pass 2 without trails (same frame) instead of failing
+            (void)hipGetLastError();
+            fp.spec = 0;
+            fp.spec_cap = 0;
+            return hipSuccess;
+        }
         fp.spec_log = (float4*)d.spec.p;
     }
     return hipSuccess;

@@ -177,6 +177,7 @@ hipError_t launch_wavefront(const DevScene& sc, const FrameParams& fp, int block
 // the device pick of pass 2 encodes "T trails" as kSpecPick + T in FrameParams::walk_team_dev
 constexpr int kSpecTrails = 8;
 constexpr int kSpecPick = 10;
+constexpr int kSpecCapMax = 256;   // records per trail log at most (FrameParams::spec_cap)
 // resident lanes per CU of the BVH2 walks (render_resume_kernel, spec_kernel: 4 waves per SIMD)
 constexpr int kWalkLanesPerCu = 4 * 4 * 64;
 size_t spec_log_bytes(const FrameParams& fp, int cus);

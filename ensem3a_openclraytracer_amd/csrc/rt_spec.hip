@@ -22,6 +22,9 @@
 // records or at a sample that draws nothing (fixed_point: every later sample repeats it).
 // So the frame is the serial one bit for bit whatever the guesses; only the work and the chain's
 // latency depend on them (tools/chain_speculation.py prices both on the CPU oracle).
+#include <mutex>
+#include <vector>
+
 #include "rt_device.h"
 
 namespace rt {
@@ -199,6 +202,9 @@ spec_kernel(DevScene S, FrameParams F, float* __restrict__ out, unsigned int* __
             sm_[u] = __shfl(s | (mode << 16), team0 + u, 64);
             dn_[u] = __shfl(D, team0 + u, 64);
         }
+        // the records those counts cover were stored by lanes of this wave in earlier iterations (release
+        // fence after each log store): the acquire keeps the log reads below after the counts were taken
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         // trail u's value, for a runtime u (a select chain: the arrays stay in registers)
         auto pick = [&](const int* a, int u) __attribute__((always_inline)) {
             int v = 0;
@@ -296,6 +302,9 @@ spec_kernel(DevScene S, FrameParams F, float* __restrict__ out, unsigned int* __
                 } else {
                     *log_at(tau, s) = make_float4(__uint_as_float((uint32_t)D | (fixed ? kFixedBit : 0u)), so.x,
                                                      so.y, so.z);
+                    // published to the wave's other trails through the count s, read by a shuffle in a later
+                    // iteration (acquire fence there): the record is ordered before that count
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
                     ++s;
                     if (fixed || s >= cap) {
                         D += dcur;
@@ -451,8 +460,22 @@ hipError_t launch_spec(const DevScene& sc, const FrameParams& fp, int block, flo
     int dev = 0, cus = 0, per_cu = 0;
     hipError_t e = hipGetDevice(&dev);
     if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    if (e == hipSuccess) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, block, lds);
     if (e != hipSuccess) return e;
+    {
+        // blocks per CU of each (instantiation, block, LDS), queried once: an automatic pass 2 launches all
+        // three trail kernels of which at most one renders, and the host query costs more than their launches
+        struct Occ { const void* fn; int block; size_t lds; int per_cu; };
+        static std::mutex mu;
+        static std::vector<Occ> seen;
+        std::lock_guard<std::mutex> g(mu);
+        for (const Occ& o : seen)
+            if (o.fn == fn && o.block == block && o.lds == lds) per_cu = o.per_cu;
+        if (per_cu == 0) {
+            e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, block, lds);
+            if (e != hipSuccess) return e;
+            seen.push_back({fn, block, lds, per_cu});
+        }
+    }
     const int cap_cu = fp.max_waves > 0 ? std::max(1, fp.max_waves * 4 * 64 / block) : INT_MAX;
     // at most kWalkLanesPerCu lanes per CU: one trail log each (spec_log_bytes)
     const int cap_logs = std::max(1, kWalkLanesPerCu / block);

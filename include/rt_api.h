@@ -50,7 +50,8 @@ enum rt_bvh_layout {
     RT_BVH_SAH = 1        /* surface-area-heuristic regrouping (default) */
 };
 
-/* Create a context on n_devices HIP devices (device_ids may be NULL = 0..n-1).
+/* Create a context on n_devices HIP devices (device_ids may be NULL = 0..n-1; explicit ids may
+ * repeat a device: each slot renders its own interleaved rows with its own stream and buffers).
  * Replaces the pyopencl Context/CommandQueue/Program build of
  * KernelLauncher.__init__ (KernelLauncher.py:8-31). */
 int rt_create(int n_devices, const int* device_ids, rt_ctx** out);

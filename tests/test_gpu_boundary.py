@@ -101,6 +101,38 @@ def test_scene_upload_waits_for_a_launch_in_flight(first, second, size):
     ctx.close()
 
 
+@pytest.mark.parametrize("slots", [2, 3])
+@pytest.mark.parametrize("case", ["cornell_128_s16", "monkey_c3_64_s4", "serre_96x54_s4"])
+def test_multi_device_launcher_deinterleaves_rows(case, slots):
+    """KernelLauncher(device=[0, 0, ...]): the single-process multi-device path of the Tk UI.  rt_render
+    launches every device slot on its interleaved rows (row r on slot r mod n, each slot with its own
+    stream and buffers -- here all on GPU 0), copies each tile back and de-interleaves the rows into the
+    caller's array (rt_api.hip render_host).  The frame, float32 and fused rgb8, is the one-device
+    frame bit for bit, including a partial last row."""
+    from ensem3a_openclraytracer_amd.KernelLauncher import KernelLauncher
+    sc, cam, env, npix, spp, mb, ibl = W.PARITY_CASES[case].inputs()
+    one = KernelLauncher(None, None, 0, None)
+    multi = KernelLauncher(None, None, [0] * slots, None)
+    try:
+        assert multi.native.n_devices == slots
+        for n in (npix, npix - int(cam[6]) // 2 - 1):
+            args = (sc.V_p, sc.V_n, sc.V_uv, sc.faceData, sc.materialData, sc.lightData, sc.BVH.exportArray,
+                    cam, env, n, spp, mb, ibl)
+            want = np.zeros(3 * n, np.float32)
+            one.launch_Raytracing(want, *args)
+            got = np.full(3 * n, -1.0, np.float32)
+            multi.launch_Raytracing(got, *args)
+            np.testing.assert_array_equal(got, want)
+            want8 = np.zeros(3 * n, np.uint8)
+            one.launch_Raytracing_rgb8(want8, *args, gamma=True)
+            got8 = np.zeros(3 * n, np.uint8)
+            multi.launch_Raytracing_rgb8(got8, *args, gamma=True)
+            np.testing.assert_array_equal(got8, want8)
+    finally:
+        one.close()
+        multi.close()
+
+
 RCCL_ONE_RANK = r'''
 import os, sys
 sys.path.insert(0, sys.argv[1])

@@ -622,6 +622,24 @@ def test_full_c2_every_pixel_vs_oracle(kl):
     assert set(bad.tolist()) <= {203399}, bad[:20]
 
 
+def test_c1_every_pixel_vs_oracle(kl):
+    """C1 (Cornell 256^2, 4 spp: BASELINE configs[0], the reference's own CPU-device case) through the
+    drop-in launch_Raytracing, every pixel against the CPU oracle: REF and FAST bit for bit; FAST's
+    team choice for this small tile (auto) and the explicit one-lane walk give the same frame."""
+    sc, cam, env, npix, spp, mb, ibl = W.CONFIGS["C1"].inputs()
+    assert (npix, spp, mb) == (256 * 256, 4, 4)
+    ora = _oracle(sc, cam, env, npix, spp, mb, ibl)
+    np.testing.assert_array_equal(_launch(kl, sc, cam, env, npix, spp, mb, ibl, "ref"), ora)
+    f = _launch(kl, sc, cam, env, npix, spp, mb, ibl, "fast")
+    compare.assert_gate(f, ora, "C1 fast vs oracle")
+    np.testing.assert_array_equal(f, ora)
+    try:
+        kl.native.set_option("team", 1)
+        np.testing.assert_array_equal(_launch(kl, sc, cam, env, npix, spp, mb, ibl, "fast"), ora)
+    finally:
+        kl.native.set_option("team", 0)
+
+
 @pytest.mark.parametrize("row_step", [8, 16])
 def test_full_c2_multi_gpu_tiles_match_one_gpu_frame(kl, row_step):
     """A rank's tile of an N-GPU C2 frame at full size (rows r::N; N=16 runs the team kernel, auto) is
@@ -856,6 +874,44 @@ def test_full_size_fast_vs_ref_pixel_counts(kl, config):
         assert set(diff.tolist()) <= pinned, (diff.size, diff[:20])
     f = frames["fast"]
     assert np.isfinite(f).all() and 0.0 <= f.min() and f.max() <= 1.0
+
+
+# C5 at its configured 1024 spp: a row sample of the frame (rows 60::64, 34 full-width rows), FAST vs REF
+# on every pixel of it, and REF vs the CPU oracle on row 700 (one of the sample's rows) bit for bit.
+# Measured non-identical FAST/REF pixels of the sample (MI355X), pinned like FULL_SIZE_FAST.
+C5_FULL_SPP_ROWS = (60, 64, 700, set())
+
+
+def test_c5_full_spp_rows_vs_ref_and_oracle(kl):
+    import json
+    import torch
+    from ensem3a_openclraytracer_amd import distributed as D
+    row0, step, orow, pinned = C5_FULL_SPP_ROWS
+    sc, cam, env, npix, spp, mb, ibl = W.CONFIGS["C5"].inputs()
+    assert spp == 1024 and (orow - row0) % step == 0
+    W_ = int(cam[6])
+    _launch(kl, sc, cam, env, npix, 1, mb, ibl, "fast")   # uploads the scene and IBL
+    rows = D.tile_rows(npix, W_, row0, step)
+    out = torch.empty(3 * W_ * rows, dtype=torch.float32, device="cuda")
+    ctx = kl.native
+    frames = {}
+    try:
+        for trav in ("ref", "fast"):
+            ctx.set_option("traversal", _native.RT_TRAVERSAL_REF if trav == "ref" else _native.RT_TRAVERSAL_FAST)
+            ctx.render_device(cam, env, npix, spp, mb, row0, step, out.data_ptr())
+            torch.cuda.synchronize()
+            frames[trav] = out.cpu().numpy().copy()
+    finally:
+        ctx.set_option("traversal", _native.RT_TRAVERSAL_FAST)
+    diff = np.unique(np.nonzero(frames["fast"] != frames["ref"])[0] // 3)
+    st = compare.assert_gate(frames["fast"], frames["ref"], "C5 1024 spp rows, FAST vs REF")
+    print(json.dumps({"config": "C5", "spp": spp, "rows": f"{row0}::{step}", "pixels": int(rows * W_),
+                      "non_identical": int(diff.size), "frac_identical": st["frac_identical"],
+                      "set": [int(x) for x in diff[:64]]}))
+    assert set(diff.tolist()) <= pinned, (diff.size, diff[:20])
+    ora = _oracle(sc, cam, env, npix, spp, mb, ibl, row0=orow, row_step=npix // W_ + 1)
+    np.testing.assert_array_equal(frames["ref"].reshape(rows, W_ * 3)[(orow - row0) // step], ora)
+    assert np.isfinite(frames["fast"]).all() and 0.0 <= frames["fast"].min() and frames["fast"].max() <= 1.0
 
 
 @pytest.mark.parametrize("case", ["monkey_c3_64_s4", "serre_96x54_s4", "proto_64_s4", "furnace_64_s4", "grid"])

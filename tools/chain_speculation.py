@@ -54,17 +54,37 @@ def pilot_mu(nd, spp, k):
     return max(seq[-1] / k, 2.0)
 
 
-def speculate(nd, nr, spp, T, mu):
+def modal_draws(nd, k):
+    """The most frequent draw count of the chain's first k samples (what a pilot pass of k samples saw)."""
+    seq = chain(nd, k)
+    vals, cnt = np.unique([int(nd[D // 2]) for D in seq], return_counts=True)
+    return int(vals[np.argmax(cnt)])
+
+
+def speculate(nd, nr, spp, T, mu, k=0, snap=0):
     """Event simulation: lanes walk trails from G_t, a lane stops on an offset already computed or
-    being computed; returns (time the chain is complete, total rays traced) in rays."""
+    being computed; returns (time the chain is complete, total rays traced) in rays.
+    k > 0: the chain's first k samples are already done (a pilot pass, rt_spec.hip): trail 0 continues
+    from their end offset D0 and trail t > 0 starts at D0 + ahead_t, ahead_t = t (spp - k) / T * mu
+    draws; snap > 0 rounds ahead_t to a multiple of snap draws (the pixel's modal draws per sample), so
+    that a trail starts on the chain's own offsets wherever the samples between D0 and it all drew
+    the modal count (C2's samples mostly draw 10)."""
     P = len(nd)
     cost = lambda p: max(int(nr[p // 2]), 1)   # noqa: E731
     done, claim, ev, work = {}, {}, [], 0
+    pre = chain(nd, k + 1) if k > 0 else [0]
+    D0 = pre[-1]
+    t0 = 0   # the pilot's samples run serially first (pass 1), their rays are work too
+    for q in dict.fromkeys(pre[:-1]):
+        t0 += cost(q)
+        done[q] = t0
+    work += t0
     for t in range(T):
-        g = int(round(t * spp / T * mu / 2)) * 2
-        if g // 2 < P and g not in claim:
+        ahead = t * (spp - k) / T * mu
+        g = D0 + (int(round(ahead / snap)) * snap if snap > 0 else int(round(ahead / 2)) * 2)
+        if g // 2 < P and g not in claim and g not in done:
             claim[g] = t
-            heapq.heappush(ev, (cost(g), t, g))
+            heapq.heappush(ev, (t0 + cost(g), t, g))
     seq = chain(nd, spp)
     tnow = 0
     while ev:
@@ -115,13 +135,25 @@ def main():
     mus = np.array([chain(nd, spp + 1)[-1] / spp for _, _, nd, _ in tr])
     print(f"{name}: {npx} pixels, draws/sample mean {mus.mean():.2f} (std {mus.std():.2f}); serial chain "
           f"mean {ser.mean():.1f} rays, max {ser.max()}")
-    for T in [int(x) for x in os.environ.get("SPEC_TRAILS", "2,3,4").split(",")]:
-        r = [speculate(nd, nr, spp, T, mu if mu > 0 else pilot_mu(nd, spp, max(spp // 8, 1)))
-             for _, _, nd, nr in tr]
-        lat = np.array([a for a, _ in r], float)
-        wk = np.array([b for _, b in r], float)
-        print(f"T={T}: latency mean {lat.mean():.1f} p99 {np.percentile(lat, 99):.1f} max {lat.max():.0f} rays "
-              f"(max {ser.max() / lat.max():.2f}x shorter than serial), work {wk.sum() / ser.sum():.3f}x")
+    k = max(spp // 8, 1)
+    modes = os.environ.get("SPEC_MODES", "static").split(",")
+    for mode in modes:
+        # static: guesses from offset 0, no pilot (r03 pricing); pilot: trails after a spp/8 pilot, as the
+        # r04 kernel runs them; snap: the pilot's guesses rounded to multiples of the modal draw count
+        for T in [int(x) for x in os.environ.get("SPEC_TRAILS", "2,3,4").split(",")]:
+            r = []
+            for _, _, nd, nr in tr:
+                m = mu if mu > 0 else pilot_mu(nd, spp, k)
+                if mode == "static":
+                    r.append(speculate(nd, nr, spp, T, m))
+                else:
+                    r.append(speculate(nd, nr, spp, T, m, k=k, snap=modal_draws(nd, k) if mode == "snap" else 0))
+            lat = np.array([a for a, _ in r], float)
+            wk = np.array([b for _, b in r], float)
+            # the pilot modes count the pilot's rays too (they are part of the tile's time)
+            print(f"{mode} T={T}: latency mean {lat.mean():.1f} p99 {np.percentile(lat, 99):.1f} max {lat.max():.0f} "
+                  f"rays (max {ser.max() / lat.max():.2f}x shorter than serial), work {wk.sum() / ser.sum():.3f}x",
+                  flush=True)
 
 
 if __name__ == "__main__":
