@@ -52,6 +52,9 @@ struct DevScene {
     const float4* wnodes;
     const float4* wleaves;
     int32_t wroot_ref;
+    // variant build RT_QNODE: the BVH2 nodes in 32 bytes (rt_api.hip emit_qnodes; leaves are wleaves),
+    // nullptr when the scene has no such layout
+    const float4* qnodes;
     float root_box[6];     // min.xyz, max.xyz of the root
     // REF traversal: the reference's own AoS export, 9 floats per node
     const float* bvh9;

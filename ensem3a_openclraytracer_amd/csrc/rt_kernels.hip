@@ -402,6 +402,12 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WIDE ?
     const char* const tb = reinterpret_cast<const char*>(tris);
     const char* const wnb = reinterpret_cast<const char*>(S.wnodes);   // WIDE: 4-wide nodes / leaf records
     const char* const wlb = reinterpret_cast<const char*>(S.wleaves);
+#ifdef RT_QNODE
+    constexpr bool QN = STEP && !WIDE && !SMEM && TS == 1;   // the 32-byte node layout (q_step)
+    const char* const qnb = reinterpret_cast<const char*>(S.qnodes);
+#else
+    constexpr bool QN = false;
+#endif
     const unsigned kstride = SMEM ? 16u * (unsigned)S.nnodes : 16u;
     const int W = F.width;
     const int imgSize = (int)F.npix;
@@ -505,7 +511,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WIDE ?
     auto start = [&](rtm_f3 o, rtm_f3 d) __attribute__((always_inline)) {
         ++cost;
         tracing = !fast_init<COUNT>(S, T, o, d, c);
-        if (WIDE) T.item = S.wroot_ref;
+        if (WIDE || QN) T.item = S.wroot_ref;   // the root, or the root leaf's 64-byte record
         if (TS > 1) {   // the team's first lane takes the root; the others steal from it
             if (!team_leader) T.item = NO_ITEM;
             boff = 0;
@@ -702,12 +708,17 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WIDE ?
         const unsigned long long alive = __ballot(phase != DONE);
         const int rthr = F.resume_min * __popcll(alive);
         while (true) {
-            if (tracing && (TS > 1 ? team_step<COUNT, SMEM, OVF>(TS, T, boff, nb, tb, lst, kstride, c)
-                            : WIDE ? (STEP ? wide_step<COUNT, OVF>(T, wnb, wlb, lst, c)
-                                           : wide_round<COUNT, OVF>(T, wnb, wlb, lst, c))
-                            : STEP ? fast_step<COUNT, SMEM, OVF>(S, T, nb, tb, lst, kstride, c)
-                                   : fast_round<COUNT, SMEM, OVF>(S, T, nb, tb, lst, kstride, c)))
-                tracing = false;
+            bool fin;
+#ifdef RT_QNODE
+            if (QN) fin = tracing && q_step<COUNT, OVF>(T, qnb, wlb, lst, c);
+            else
+#endif
+            fin = tracing && (TS > 1 ? team_step<COUNT, SMEM, OVF>(TS, T, boff, nb, tb, lst, kstride, c)
+                              : WIDE ? (STEP ? wide_step<COUNT, OVF>(T, wnb, wlb, lst, c)
+                                             : wide_round<COUNT, OVF>(T, wnb, wlb, lst, c))
+                              : STEP ? fast_step<COUNT, SMEM, OVF>(S, T, nb, tb, lst, kstride, c)
+                                     : fast_round<COUNT, SMEM, OVF>(S, T, nb, tb, lst, kstride, c));
+            if (fin) tracing = false;
             const unsigned long long tr = __ballot(tracing);
             if (tr == 0 || 64 * __popcll(alive & ~tr) >= rthr) break;
         }
