@@ -50,10 +50,11 @@ struct Device {
     hipStream_t stream = nullptr;
     int cus = 0;                  // compute units (sizes the FAST stack overflow buffer)
     DevBuf stack_ovf;             // FAST traversal stack entries beyond the LDS part
-    DevBuf nodes, qnodes, wnodes, wleaves, tri_fast, brute, brute_box, bvh9, tri_geo, tri_shade, tri_frame, mat, ibl, ibl_sum, out, out8, counts, work, scratch_a, scratch_b;
+    DevBuf nodes, wnodes, wleaves, tri_fast, brute, brute_box, bvh9, tri_geo, tri_shade, tri_frame, mat, ibl, ibl_sum, out, out8, counts, work, scratch_a, scratch_b;
     DevBuf pilot;                 // two-pass launches: per-pixel state, cost and order (FrameParams::pilot_*)
     DevBuf wf;                    // wavefront launches: the waves' path-state regions (FrameParams::wf_buf)
     DevBuf spec;                  // speculation: the trails' sample logs (FrameParams::spec_log)
+    DevBuf slice;                 // sample slices: per-pixel state + samples done (FrameParams::slice_*)
     char* host_stage = nullptr;   // pinned staging for rt_render / rt_render_rgb8
     size_t host_stage_bytes = 0;
     // Every launch of this context on the device shares `work` (pixel counters + launch constants)
@@ -68,7 +69,6 @@ struct Device {
 // Host copy of the packed scene (kept to upload on every device).
 struct HostScene {
     std::vector<float> nodes;      // 16 floats per internal node
-    std::vector<float> qnodes;     // variant build RT_QNODE: 8 floats per internal node (DevScene::qnodes)
     std::vector<float> wnodes;     // wide layout: 16 floats per 4-wide node (DevScene::wnodes)
     std::vector<float> wleaves;    // wide layout: 16 floats per leaf, in reference DFS rank order
     int32_t nwnodes = 0, wroot_ref = 0, wdepth = 1;
@@ -119,6 +119,7 @@ struct rt_ctx {
     int wf_refill = 0;    // wavefront trace phase: idle lanes that trigger a refill (0 = auto)
     int spec = -1;        // small tiles: speculative trails per pixel in pass 2 (0 = off, 2, 4 or 8, -1 = auto)
     int handout = -1;     // pixel hand-out: 0 = interleaved chunks, 1 = a contiguous block per XCD group, -1 = auto
+    int slices = -1;      // one-pass tree-walk launches: sample slices per pixel (FrameParams::slices; 0 off, -1 auto)
     std::string err;
 };
 
@@ -344,46 +345,6 @@ void emit_wide(HostScene& hs, const int32_t* L, const int32_t* R, const int32_t*
     hs.wdepth = bfs.empty() ? 1 : std::max(1, need[0]);
 }
 
-// The BVH2 nodes in 32 bytes (DevScene::qnodes, variant build RT_QNODE; rt_device.h q_step), from the
-// 64-byte nodes and the 4-wide layout's leaf records (wleaves, reference DFS rank order):
-//   float4 (p.x, p.y, p.z, ex | ey << 8 | ez << 16 | refB[19:12] << 24)   p = the children's lower corner
-//   uint4  bytes (lo0.x lo0.y lo0.z hi0.x | hi0.y hi0.z lo1.x lo1.y | lo1.z hi1.x hi1.y hi1.z | refA | refB[11:0] << 20)
-// child refs of 20 bits: < 2^19 node index, else 2^19 + the leaf's rank.  Bounds as emit_wide's.  No
-// layout (empty) for trees or triangle counts of 2^19 and more or without leaf records.
-void emit_qnodes(HostScene& hs) {
-    hs.qnodes.clear();
-#ifdef RT_QNODE
-    constexpr uint32_t kLeaf = 1u << 19;
-    if (hs.wleaves.empty() || hs.nnodes <= 0 || hs.nnodes >= (int32_t)kLeaf || hs.ntri >= (int32_t)kLeaf) return;
-    std::vector<float> q((size_t)hs.nnodes * 8, 0.0f);
-    auto qref = [&](int32_t r) -> uint32_t {   // 64-byte node ref or ~(48 * tri_fast record) -> 20 bits
-        return r >= 0 ? (uint32_t)r : kLeaf + (uint32_t)as_i32(hs.tri_fast[12 * (size_t)((~r) / 48) + 3]);
-    };
-    auto pack = [](uint32_t a, uint32_t b, uint32_t c, uint32_t d) { return as_f32((int32_t)(a | b << 8 | c << 16 | d << 24)); };
-    for (int32_t w = 0; w < hs.nnodes; ++w) {
-        const float* o = hs.nodes.data() + 16 * (size_t)w;
-        float lo[3][2] = {{o[0], o[4]}, {o[2], o[6]}, {o[8], o[10]}};
-        float hi[3][2] = {{o[1], o[5]}, {o[3], o[7]}, {o[9], o[11]}};
-        uint8_t ql[3][2] = {}, qh[3][2] = {};
-        uint32_t meta = 0;
-        float* out = q.data() + 8 * (size_t)w;
-        for (int a = 0; a < 3; ++a) {
-            out[a] = std::min(lo[a][0], lo[a][1]);
-            const int ex = rt_debug_quantise_axis(out[a], lo[a], hi[a], 2, ql[a], qh[a]);
-            if (ex < 0) return;   // no containing quantisation: no 32-byte layout
-            meta |= (uint32_t)ex << (8 * a);
-        }
-        const uint32_t ra = qref(as_i32(o[12])), rb = qref(as_i32(o[13]));
-        out[3] = as_f32((int32_t)(meta | (rb >> 12) << 24));
-        out[4] = pack(ql[0][0], ql[1][0], ql[2][0], qh[0][0]);
-        out[5] = pack(qh[1][0], qh[2][0], ql[0][1], ql[1][1]);
-        out[6] = pack(ql[2][1], qh[0][1], qh[1][1], qh[2][1]);
-        out[7] = as_f32((int32_t)(ra | (rb & 0xfffu) << 20));
-    }
-    hs.qnodes.swap(q);
-#endif
-}
-
 // Emit the FAST node array from a binary tree with one triangle per leaf: internal nodes in BFS
 // order, each holding its two children's boxes and refs (rt_internal.h DevScene::nodes).
 // box: 6 floats per tree node (lo.xyz, hi.xyz).
@@ -455,7 +416,6 @@ void emit_bvh(HostScene& hs, const int32_t* L, const int32_t* R, const int32_t* 
     for (int k = 0; k < 6; ++k) hs.root_box[k] = box[k];
     hs.depth = bfs.empty() ? 1 : std::max(1, need[0]);
     emit_wide(hs, L, R, T, box, nn);
-    emit_qnodes(hs);
 }
 
 // Pack the FAST layout from the reference export.  Returns false (with
@@ -683,13 +643,6 @@ rt::DevScene dev_scene(const rt_ctx* ctx, const Device& d) {
     s.wnodes = wide ? (const float4*)d.wnodes.p : nullptr;
     s.wleaves = wide ? (const float4*)d.wleaves.p : nullptr;
     s.wroot_ref = ctx->hs.wroot_ref;
-    s.qnodes = nullptr;
-#ifdef RT_QNODE
-    if (!wide && !ctx->hs.qnodes.empty()) {   // the BVH2 item step walks the 32-byte nodes + 64-byte leaves
-        s.qnodes = (const float4*)d.qnodes.p;
-        s.wleaves = (const float4*)d.wleaves.p;
-    }
-#endif
     for (int k = 0; k < 6; ++k) s.root_box[k] = ctx->hs.root_box[k];
     s.bvh9 = (const float*)d.bvh9.p;
     s.nbvh9 = ctx->hs.nbvh9;
@@ -746,9 +699,6 @@ int check_frame(rt_ctx* ctx, const float* cam, const float* env, int64_t npix, i
     fp->log_pixel = -1;
     fp->resume_min = ctx->resume_min >= 0 ? ctx->resume_min : use_wide(ctx) ? kResumeMinWide : kResumeMinBvh2;
     fp->step = ctx->step;
-#ifdef RT_QNODE
-    if (ctx->hs.qnodes.empty()) fp->step = 2;   // the variant's item step walks only the 32-byte layout
-#endif
     fp->sun_skip = (ctx->sun_skip && env[3] == 0.0f && env[4] >= 0.0f && ctx->hs.colors_finite) ? 1 : 0;
     fp->sun_any = (ctx->sun_any && !ctx->hs.has_glass) ? 1 : 0;
     fp->wide = use_wide(ctx) ? 1 : 0;
@@ -763,6 +713,9 @@ int check_frame(rt_ctx* ctx, const float* cam, const float* env, int64_t npix, i
     fp->spec = 0;
     fp->spec_log = nullptr;
     fp->spec_cap = 0;
+    fp->slices = 0;
+    fp->slice_state = nullptr;
+    fp->slice_ready = nullptr;
     fp->walk_team_dev = nullptr;
     fp->pilot_cost = nullptr;
     fp->pilot_order = nullptr;
@@ -832,8 +785,8 @@ void rt_destroy(rt_ctx* ctx) {
         if (hipSetDevice(d.id) != hipSuccess) continue;
         if (d.pending) (void)hipEventSynchronize(d.done);
         if (d.stream) (void)hipStreamSynchronize(d.stream);
-        for (DevBuf* b : {&d.stack_ovf, &d.nodes, &d.qnodes, &d.wnodes, &d.wleaves, &d.tri_fast, &d.brute, &d.brute_box, &d.bvh9, &d.tri_geo, &d.tri_shade, &d.tri_frame, &d.mat, &d.ibl, &d.ibl_sum, &d.out,
-                          &d.out8, &d.counts, &d.work, &d.scratch_a, &d.scratch_b, &d.pilot, &d.wf, &d.spec})
+        for (DevBuf* b : {&d.stack_ovf, &d.nodes, &d.wnodes, &d.wleaves, &d.tri_fast, &d.brute, &d.brute_box, &d.bvh9, &d.tri_geo, &d.tri_shade, &d.tri_frame, &d.mat, &d.ibl, &d.ibl_sum, &d.out,
+                          &d.out8, &d.counts, &d.work, &d.scratch_a, &d.scratch_b, &d.pilot, &d.wf, &d.spec, &d.slice})
             release(*b);
         if (d.host_stage) (void)hipHostFree(d.host_stage);
         if (d.stream) (void)hipStreamDestroy(d.stream);
@@ -871,7 +824,6 @@ int rt_set_option(rt_ctx* ctx, const char* key, int64_t value) {
             // a launch in flight on another stream may still read the buffers upload() can free
             HIP_OR_RET(ctx, hipStreamSynchronize(d.stream));
             HIP_OR_RET(ctx, upload(d.nodes, hs.nodes, d.stream));
-        HIP_OR_RET(ctx, upload(d.qnodes, hs.qnodes, d.stream));
             HIP_OR_RET(ctx, upload(d.wnodes, hs.wnodes, d.stream));
             HIP_OR_RET(ctx, upload(d.wleaves, hs.wleaves, d.stream));
             HIP_OR_RET(ctx, upload(d.brute, hs.brute, d.stream));
@@ -960,6 +912,11 @@ int rt_set_option(rt_ctx* ctx, const char* key, int64_t value) {
     if (!std::strcmp(key, "ref_stack")) {
         if (value < 20 || value > 64) return set_err(ctx, RT_ERR_ARG, "ref_stack must be in 20..64 (20 = the reference's)");
         ctx->ref_stack = (int)value;
+        return RT_OK;
+    }
+    if (!std::strcmp(key, "slices")) {
+        if (value < -1 || value > 16) return set_err(ctx, RT_ERR_ARG, "slices must be -1 (auto), 0 (off) or 1..16");
+        ctx->slices = (int)value;
         return RT_OK;
     }
     if (!std::strcmp(key, "handout")) {
@@ -1082,7 +1039,6 @@ int rt_set_scene(rt_ctx* ctx, const float* vp, int64_t nvp, const float* vn, int
         // a launch in flight on another stream may still read the buffers upload() / ensure() free
         HIP_OR_RET(ctx, hipStreamSynchronize(d.stream));
         HIP_OR_RET(ctx, upload(d.nodes, hs.nodes, d.stream));
-        HIP_OR_RET(ctx, upload(d.qnodes, hs.qnodes, d.stream));
         HIP_OR_RET(ctx, upload(d.wnodes, hs.wnodes, d.stream));
         HIP_OR_RET(ctx, upload(d.wleaves, hs.wleaves, d.stream));
         HIP_OR_RET(ctx, upload(d.brute, hs.brute, d.stream));
@@ -1208,6 +1164,35 @@ hipError_t setup_pilot(rt_ctx* ctx, Device& d, rt::FrameParams& fp) {
 }  // namespace
 
 namespace {
+// Sample slices (FrameParams::slices; option "slices": -1 auto, 0 or 1 off, K): one-pass launches of the
+// resumable tree walk hand out each pixel's samples as K slices, slice-major, so that a tile ends on a
+// slice rather than on a whole pixel.  Auto: on the 4-wide walk (C5, whose pixels are all about equally
+// long: a tile of n pixels per resident lane ends after ceil(n) pixel times, 2.26 -> 3 on an eighth of
+// C5), K = kSlicesWide.  Sets fp's slice fields, sizes the device's state buffer and zeroes the
+// samples-done words on stream s (the launch's stream).
+constexpr int kSlicesWide = 4;
+hipError_t setup_slices(rt_ctx* ctx, Device& d, rt::FrameParams& fp, hipStream_t s) {
+    fp.slices = 0;
+    if (fp.pilot > 0 || fp.wf_buf || effective_traversal(ctx) != RT_TRAVERSAL_FAST || fp.nloc <= 0 ||
+        ctx->hs.nbrute > 0 || fp.resume_min <= 0 || ctx->slices == 0)
+        return hipSuccess;
+    int k = ctx->slices > 0 ? ctx->slices : (use_wide(ctx) ? kSlicesWide : 1);
+    k = std::min(k, fp.spp / 2);   // every slice at least two samples
+    if (k <= 1 || (int64_t)fp.nloc * k >= ((int64_t)1 << 32)) return hipSuccess;
+    const size_t n = (size_t)fp.nloc;
+    const size_t need = n * 32 + n * sizeof(uint32_t);
+    hipError_t e = hipSuccess;
+    // growing frees the old buffer from the host: the last launch (any stream) may still use it
+    if (d.slice.bytes < need && d.pending) e = hipEventSynchronize(d.done);
+    if (e == hipSuccess) e = ensure(d.slice, need);
+    if (e == hipSuccess) e = hipMemsetAsync((char*)d.slice.p + n * 32, 0, n * sizeof(uint32_t), s);
+    if (e != hipSuccess) return e;
+    fp.slices = k;
+    fp.slice_state = (float4*)d.slice.p;
+    fp.slice_ready = (uint32_t*)((char*)d.slice.p + n * 32);
+    return hipSuccess;
+}
+
 // Wavefront launches (FrameParams::wf_slots): size the device's path-state regions, or fall back to
 // the megakernel (wf_slots = 0) where the launch cannot take the wavefront walk
 hipError_t setup_wavefront(rt_ctx* ctx, Device& d, rt::FrameParams& fp) {
@@ -1248,6 +1233,7 @@ int rt_render_device(rt_ctx* ctx, int device_index, const float cam[10], const f
     HIP_OR_RET(ctx, order_after_last(d, s));
     HIP_OR_RET(ctx, setup_wavefront(ctx, d, fp));
     HIP_OR_RET(ctx, setup_pilot(ctx, d, fp));
+    HIP_OR_RET(ctx, setup_slices(ctx, d, fp, s));
     HIP_OR_RET(ctx, rt::launch_render(dev_scene(ctx, d), fp, effective_traversal(ctx), ctx->block, d_out, nullptr,
                                       (unsigned int*)d.work.p, s));
     HIP_OR_RET(ctx, mark_launch(d, s));
@@ -1316,6 +1302,7 @@ int render_host(rt_ctx* ctx, const float cam[10], const float env[5], int64_t np
         HIP_OR_RET(ctx, order_after_last(d, d.stream));
         HIP_OR_RET(ctx, setup_wavefront(ctx, d, fp));
         HIP_OR_RET(ctx, setup_pilot(ctx, d, fp));
+        HIP_OR_RET(ctx, setup_slices(ctx, d, fp, d.stream));
         HIP_OR_RET(ctx, rt::launch_render(dev_scene(ctx, d), fp, effective_traversal(ctx), ctx->block,
                                           (float*)d.out.p, nullptr, (unsigned int*)d.work.p, d.stream));
         HIP_OR_RET(ctx, mark_launch(d, d.stream));

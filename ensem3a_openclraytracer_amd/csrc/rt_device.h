@@ -816,6 +816,11 @@ __device__ __forceinline__ void store_pixel(float* __restrict__ out, int p, rtm_
 }
 
 enum Phase { FETCH = 0, PRIMARY = 1, PREP = 2, BOUNCE = 3, SUN = 4, DONE = 5 };
+// a job of sample slice k > 0 waiting for slice k - 1 of its pixel (FrameParams::slices)
+constexpr int WAIT_SLICE = 7;
+// words other workgroups read or write within a launch: global address space, agent-scope accesses
+typedef unsigned __attribute__((address_space(1))) gu32;
+typedef unsigned long long __attribute__((address_space(1))) gu64;
 
 // ---- pixel hand-out ----
 // Tile pixels are dealt in chunks of 2^kChunkShift consecutive pixels: chunk c belongs to group
@@ -853,13 +858,17 @@ __device__ __forceinline__ unsigned group_pixels(unsigned g, unsigned nloc, unsi
 // leader.  Returns the calling lane's tile pixel index (>= nloc: none left in the tile).  Called
 // with the whole wave active; all control flow is wave-uniform, and the requests are served in
 // rank order (group by group), so a lane only needs its rank.
+// slices > 1 (FrameParams::slices): a group hands out `slices` passes over its pixels, slice-major --
+// the job after its pixels' slice k is their slice k + 1 -- and the return value is the job
+// k * nloc + pixel (>= slices * nloc: none left).
 __device__ __forceinline__ unsigned take_pixel(PixelQueue& Q, unsigned long long need, int lane0,
-                                               unsigned* __restrict__ counters, unsigned nloc, int lane) {
+                                               unsigned* __restrict__ counters, unsigned nloc, int lane,
+                                               unsigned slices = 1) {
     const bool mine = (need >> lane0) & 1ull;
     const unsigned rank = (unsigned)__popcll(need & ((1ull << lane0) - 1ull));
     const unsigned total = (unsigned)__popcll(need);
     const int leader = __ffsll((long long)need) - 1;
-    unsigned q = nloc;
+    unsigned q = nloc * slices;
     unsigned base = 0;   // requests served so far
     unsigned g = blockIdx.x % (unsigned)kGroups;
     for (int t = 0; t < kGroups && base < total; ++t, g = (g + 1u) % (unsigned)kGroups) {
@@ -868,9 +877,13 @@ __device__ __forceinline__ unsigned take_pixel(PixelQueue& Q, unsigned long long
         unsigned got = 0;
         if (lane == leader) got = atomicAdd(counters + g * (unsigned)(kCounterStride / 4), k);
         const unsigned j0 = (unsigned)__builtin_amdgcn_readfirstlane((int)__shfl(got, leader, 64));
-        const unsigned have = group_pixels(g, nloc, Q.per);
+        const unsigned px = group_pixels(g, nloc, Q.per);
+        const unsigned have = px * slices;
         const unsigned nok = j0 < have ? min(have - j0, k) : 0u;
-        if (mine && rank >= base && rank < base + nok) q = group_pixel(g, j0 + (rank - base), Q.per);
+        if (mine && rank >= base && rank < base + nok) {
+            const unsigned jj = j0 + (rank - base);
+            q = slices == 1 ? group_pixel(g, jj, Q.per) : (jj / px) * nloc + group_pixel(g, jj % px, Q.per);
+        }
         if (nok < k) Q.dry |= 1u << g;   // the group's sequence has run past the tile
         base += nok;
     }
@@ -1272,82 +1285,6 @@ __device__ __forceinline__ bool wide_step(FastRay& R, const char* nb, const char
     }
     return true;
 }
-
-#ifdef RT_QNODE
-// One item of the walk over the 32-byte quantised BVH2 layout (DevScene::qnodes, rt_api.hip emit_qnodes;
-// variant build RT_QNODE): a node is half of fast_step's 64-byte record -- the two child boxes as bytes
-// against the children's lower corner p (p + q * 2^e per bound, a superset of each exact box, as the
-// 4-wide layout) and 20-bit child refs -- fetched with two 16-byte loads; a leaf is the 4-wide layout's
-// 64-byte record (exact leaf box, a.p, e1, e2, triangle index; ref ~(64 * rank)), whose two further loads
-// only leaf lanes issue.  One slab serves a node lane's child 0 and a leaf lane's exact box (wide_step).
-// The accepted triangles are fast_step's (exact leaf box passes, MT hit, k > 1e-4, lowest (k, rank)).
-constexpr unsigned kQLeafBit = 1u << 19;   // a 20-bit child ref: < 2^19 node index, else 2^19 + leaf rank
-__device__ __forceinline__ int q_ref(unsigned r) {
-    return r < kQLeafBit ? (int)r : ~(int)(64u * (r - kQLeafBit));
-}
-template <bool COUNT, bool OVF>
-__device__ __forceinline__ bool q_step(FastRay& R, const char* nb, const char* lb, const LaneStack& st, Cnt& c) {
-    const bool node = R.item >= 0;
-    const char* p = node ? nb + 32u * (unsigned)R.item : lb + ~(unsigned)R.item;
-    const float4 g0 = *reinterpret_cast<const float4*>(p);
-    const float4 g1 = *reinterpret_cast<const float4*>(p + 16);
-    float4 g2 = g1, g3 = g1;
-    if (!node) {
-        g2 = *reinterpret_cast<const float4*>(p + 32);
-        g3 = *reinterpret_cast<const float4*>(p + 48);
-    }
-    if (COUNT) count_wave(c.wave_trav);
-    const unsigned meta = __float_as_uint(g0.w);
-    const float sx = __uint_as_float((meta & 255u) << 23);
-    const float sy = __uint_as_float(((meta >> 8) & 255u) << 23);
-    const float sz = __uint_as_float(((meta >> 16) & 255u) << 23);
-    const unsigned w4 = __float_as_uint(g1.x), w5 = __float_as_uint(g1.y), w6 = __float_as_uint(g1.z),
-                   w7 = __float_as_uint(g1.w);
-    // p + q * s with q * s exact: one correctly rounded fma is the builder's bound bit for bit
-    auto dq = [](float pp, unsigned w, int b, float sc) { return fmaf((float)((w >> (8 * b)) & 255u), sc, pp); };
-    const float cull = R.bk * CULL_MARGIN;
-    float tn0, tx0, tn1, tx1;
-    slab(node ? dq(g0.x, w4, 0, sx) : g0.x, node ? dq(g0.x, w4, 3, sx) : g0.w, node ? dq(g0.y, w4, 1, sy) : g0.y,
-         node ? dq(g0.y, w5, 0, sy) : g1.x, node ? dq(g0.z, w4, 2, sz) : g0.z, node ? dq(g0.z, w5, 1, sz) : g1.y, R.o,
-         R.ix, R.iy, R.iz, tn0, tx0);
-    slab(dq(g0.x, w5, 2, sx), dq(g0.x, w6, 1, sx), dq(g0.y, w5, 3, sy), dq(g0.y, w6, 2, sy), dq(g0.z, w6, 0, sz),
-         dq(g0.z, w6, 3, sz), R.o, R.ix, R.iy, R.iz, tn1, tx1);
-    const bool b0 = box_hit(tn0, tx0, cull);
-    const bool h0 = node && b0, h1 = node && box_hit(tn1, tx1, cull);
-    const int ea = q_ref(w7 & 0xfffffu), eb = q_ref((w7 >> 20) | ((meta >> 24) << 12));
-    float k;
-    const int rank = (int)((~(unsigned)R.item) >> 6);
-    const bool mt = mt_core(rtm_v3(g1.z, g1.w, g2.x), rtm_v3(g2.y, g2.z, g2.w), rtm_v3(g3.x, g3.y, g3.z), R.o, R.d, &k);
-    const bool take = !node & b0 & mt & (k > 0.0001f) & ((k < R.bk) | ((k == R.bk) & (rank < R.brank)));
-    if (COUNT) {
-        if (node) { c.nodes++; c.boxes += 2; }
-        else { c.tris++; c.boxes++; }
-    }
-    R.bk = take ? k : R.bk;
-    R.bt = take ? 48 * __float_as_int(g3.w) : R.bt;   // the triangle's reference index
-    R.brank = take ? rank : R.brank;
-    const bool first0 = tn0 <= tn1;
-    if (h0 && h1) {   // the farther child waits on the stack
-        st.template put<OVF>(R.soff, make_int2(first0 ? eb : ea, __float_as_int(first0 ? tn1 : tn0)));
-        R.soff += st.stride;
-    }
-    const int next = (h0 && h1) ? (first0 ? ea : eb) : h0 ? ea : h1 ? eb : INT_MIN;
-    if (take && R.any) return true;
-    if (next != INT_MIN) {
-        R.item = next;
-        return false;
-    }
-    while (R.soff > 0) {   // pop the next item still in front of the best hit
-        R.soff -= st.stride;
-        const int2 en = st.template get<OVF>(R.soff);
-        if (__int_as_float(en.y) <= R.bk * CULL_MARGIN) {
-            R.item = en.x;
-            return false;
-        }
-    }
-    return true;
-}
-#endif
 
 // One round of the wide walk (the counterpart of fast_round): descend nearest children until a
 // leaf is reached or nothing is hit, test the leaf, then pop the next live entry.

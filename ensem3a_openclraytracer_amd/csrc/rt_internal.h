@@ -52,9 +52,6 @@ struct DevScene {
     const float4* wnodes;
     const float4* wleaves;
     int32_t wroot_ref;
-    // variant build RT_QNODE: the BVH2 nodes in 32 bytes (rt_api.hip emit_qnodes; leaves are wleaves),
-    // nullptr when the scene has no such layout
-    const float4* qnodes;
     float root_box[6];     // min.xyz, max.xyz of the root
     // REF traversal: the reference's own AoS export, 9 floats per node
     const float* bvh9;
@@ -144,6 +141,15 @@ struct FrameParams {
     int32_t spec;
     float4* spec_log;
     int32_t spec_cap;
+    // Sample slices (option "slices", one-pass launches of the tree walk): each pixel's samples are
+    // `slices` jobs of spp / slices samples, handed out slice-major (take_pixel), so a lane's last job
+    // is a slice, not a whole pixel: the frame's tail shrinks by that factor.  A job that ends a slice
+    // stores the pixel's state (slice_state: acc.xyz | kc, seed0 seed1 tc s; write-through) and then the
+    // samples done (slice_ready); the job of the next slice, on any lane, waits for that count and
+    // continues from the state.  Every pixel's samples run in order: the frame is the one-pass frame.
+    int32_t slices;
+    float4* slice_state;
+    uint32_t* slice_ready;
     const uint32_t* pilot_order;
     // Wavefront launches (rt_wavefront.hip, option "wavefront"): the tree walk split into a trace phase
     // and a shade phase per wave, every path's state in HBM between them.  wf_slots = path slots per

@@ -402,12 +402,6 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WIDE ?
     const char* const tb = reinterpret_cast<const char*>(tris);
     const char* const wnb = reinterpret_cast<const char*>(S.wnodes);   // WIDE: 4-wide nodes / leaf records
     const char* const wlb = reinterpret_cast<const char*>(S.wleaves);
-#ifdef RT_QNODE
-    constexpr bool QN = STEP && !WIDE && !SMEM && TS == 1;   // the 32-byte node layout (q_step)
-    const char* const qnb = reinterpret_cast<const char*>(S.qnodes);
-#else
-    constexpr bool QN = false;
-#endif
     const unsigned kstride = SMEM ? 16u * (unsigned)S.nnodes : 16u;
     const int W = F.width;
     const int imgSize = (int)F.npix;
@@ -445,6 +439,10 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WIDE ?
     bool drew = false;   // the current sample has drawn random numbers (a diffuse or glossy bounce)
     int cost = 0;        // pass 1: rays this pixel traced (pilot_cost)
     int ndraw = 0;       // pass 1, BVH2 walk: random numbers the pixel drew (its RNG offset, pilot_draws)
+    // sample slices (FrameParams::slices): the sample count this job stops at; while the job waits for the
+    // slice before it (phase WAIT_SLICE), the job's slice index
+    const unsigned nsl = (TS == 1 && F.slices > 1 && F.pass == 0) ? (unsigned)F.slices : 1u;
+    int lim = spp;
     // The deterministic prefix of the pixel's samples (FrameParams::fixed_point; BVH2 walk): a sample's
     // path up to its first diffuse or glossy bounce draws no random number -- it is the cached camera
     // hit followed by straight-through glass bounces (Raytracing.cl:72-77) -- so it is the same path in
@@ -477,14 +475,33 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WIDE ?
         F.pilot_cost[p] = s >= spp ? 0u : (unsigned)cost;
         if (!WIDE && F.pilot_draws) F.pilot_draws[p] = (uint32_t)ndraw;
     };
+    // slices: the pixel's state after this job's slice, stored write-through (sc1) for the lane that runs the
+    // next slice; then, once the wave's stores have completed, the samples done (the word that lane polls)
+    auto save_slice = [&]() __attribute__((always_inline)) {
+        if (!team_leader) return;
+        gu64* st = (gu64*)(F.slice_state + 2 * (int64_t)p);
+        auto pk = [](float a, float b) { return (unsigned long long)__float_as_uint(a) | ((unsigned long long)__float_as_uint(b) << 32); };
+        __hip_atomic_store(st + 0, pk(acc.x, acc.y), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(st + 1, pk(acc.z, kc), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(st + 2, (unsigned long long)seed0 | ((unsigned long long)seed1 << 32), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(st + 3, (unsigned long long)(unsigned)tc | ((unsigned long long)(unsigned)s << 32),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __hip_atomic_store((gu32*)(F.slice_ready + p), (unsigned)s, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+    };
     auto finish_sample = [&]() __attribute__((always_inline)) {  // output += baseColor; next sample from the cached camera hit
         if (LOG && logme) log_event(F, 3.0f, s + 1, rtm_v3(0, 0, 0), rtm_v3(0, 0, 0), 0.0f, 0, so);
         acc = rtm_add(acc, so);
         if (COUNT) c.samples++;
         ++s;
         if (s >= spp) write_pixel();
-        const bool stop = F.pass == 1 && (s >= spp || s >= F.pilot);
-        if (stop) save_pilot();
+        const bool stop = (F.pass == 1 && (s >= spp || s >= F.pilot)) || (nsl > 1 && s >= lim);
+        if (stop) {
+            if (nsl > 1) save_slice();
+            else save_pilot();
+        }
         // the next sample restarts from the cached camera hit; written as selects so that no branch
         // ends in a store the compiler could merge with the pixel store (that would force the path
         // state into scratch memory through a generic pointer)
@@ -511,7 +528,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WIDE ?
     auto start = [&](rtm_f3 o, rtm_f3 d) __attribute__((always_inline)) {
         ++cost;
         tracing = !fast_init<COUNT>(S, T, o, d, c);
-        if (WIDE || QN) T.item = S.wroot_ref;   // the root, or the root leaf's 64-byte record
+        if (WIDE) T.item = S.wroot_ref;
         if (TS > 1) {   // the team's first lane takes the root; the others steal from it
             if (!team_leader) T.item = NO_ITEM;
             boff = 0;
@@ -524,8 +541,10 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WIDE ?
         // -- refill: ballot the lanes that need a pixel, one atomic per wave (one pixel per team) --
         const unsigned long long need = __ballot(phase == FETCH) & team_leaders;
         if (need) {
-            const unsigned int q = take_pixel(pq, need, team_lane0, work_counter, nloc, lane);
+            const unsigned int qj = take_pixel(pq, need, team_lane0, work_counter, nloc, lane, nsl);
             if (phase == FETCH) {
+                const unsigned sl = qj / nloc;   // the job's slice (>= nsl: none left)
+                const unsigned q = sl < nsl ? qj - sl * nloc : nloc;
                 bool ok = q < nloc;
                 if (ok) {
                     p = F.pass == 2 ? (int)F.pilot_order[q] : (int)q;
@@ -559,7 +578,11 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WIDE ?
                         so = rtm_v3(1, 1, 1);
                         drew = false;
                         phase = s >= spp ? FETCH : PREP;   // finished in pass 1: already written
+                    } else if (sl > 0) {
+                        lim = (int)sl;   // continues the pixel once slice sl - 1 is done (below)
+                        phase = WAIT_SLICE;
                     } else {
+                        lim = (int)(((unsigned)spp) / nsl);
                         start(C.position, cd);
                     }
                 } else {
@@ -568,7 +591,34 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WIDE ?
                 }
             }
         }
+        if (nsl > 1 && phase == WAIT_SLICE) {
+            // slices: the previous slice's samples done, published by the lane that ran it (save_slice); its
+            // state is read with sc1 loads (past this CU's L1) once the count is there
+            const unsigned need_s = (unsigned)(lim * spp) / nsl;
+            const unsigned done_s = __hip_atomic_load((gu32*)(F.slice_ready + p), __ATOMIC_RELAXED,
+                                                      __HIP_MEMORY_SCOPE_AGENT);
+            if (done_s >= need_s) {
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // the state loads stay after the poll
+                gu64* st = (gu64*)(F.slice_state + 2 * (int64_t)p);
+                const unsigned long long a = __hip_atomic_load(st + 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                const unsigned long long b = __hip_atomic_load(st + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                const unsigned long long d = __hip_atomic_load(st + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                const unsigned long long e = __hip_atomic_load(st + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                acc = rtm_v3(__uint_as_float((unsigned)a), __uint_as_float((unsigned)(a >> 32)), __uint_as_float((unsigned)b));
+                kc = __uint_as_float((unsigned)(b >> 32));
+                seed0 = (uint32_t)d;
+                seed1 = (uint32_t)(d >> 32);
+                tc = (int)(unsigned)e;
+                s = (int)(unsigned)(e >> 32);
+                tri = tc; j = 0;
+                so = rtm_v3(1, 1, 1);
+                drew = false;
+                lim = (int)((unsigned)(lim + 1) * (unsigned)spp / nsl);
+                phase = s >= spp ? FETCH : PREP;   // finished early (a sample that draws nothing): written
+            }
+        }
         if (__all(phase == DONE)) break;
+        if (nsl > 1 && __all(phase == DONE || phase == WAIT_SLICE)) __builtin_amdgcn_s_sleep(8);
         if (COUNT && lane == 0) c.wave_outer++;
 
         // -- advance every lane without a ray in flight until it needs one --
@@ -708,17 +758,12 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WIDE ?
         const unsigned long long alive = __ballot(phase != DONE);
         const int rthr = F.resume_min * __popcll(alive);
         while (true) {
-            bool fin;
-#ifdef RT_QNODE
-            if (QN) fin = tracing && q_step<COUNT, OVF>(T, qnb, wlb, lst, c);
-            else
-#endif
-            fin = tracing && (TS > 1 ? team_step<COUNT, SMEM, OVF>(TS, T, boff, nb, tb, lst, kstride, c)
-                              : WIDE ? (STEP ? wide_step<COUNT, OVF>(T, wnb, wlb, lst, c)
-                                             : wide_round<COUNT, OVF>(T, wnb, wlb, lst, c))
-                              : STEP ? fast_step<COUNT, SMEM, OVF>(S, T, nb, tb, lst, kstride, c)
-                                     : fast_round<COUNT, SMEM, OVF>(S, T, nb, tb, lst, kstride, c));
-            if (fin) tracing = false;
+            if (tracing && (TS > 1 ? team_step<COUNT, SMEM, OVF>(TS, T, boff, nb, tb, lst, kstride, c)
+                            : WIDE ? (STEP ? wide_step<COUNT, OVF>(T, wnb, wlb, lst, c)
+                                           : wide_round<COUNT, OVF>(T, wnb, wlb, lst, c))
+                            : STEP ? fast_step<COUNT, SMEM, OVF>(S, T, nb, tb, lst, kstride, c)
+                                   : fast_round<COUNT, SMEM, OVF>(S, T, nb, tb, lst, kstride, c)))
+                tracing = false;
             const unsigned long long tr = __ballot(tracing);
             if (tr == 0 || 64 * __popcll(alive & ~tr) >= rthr) break;
         }

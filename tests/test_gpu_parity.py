@@ -1194,6 +1194,43 @@ def test_speculative_trails_row_tiles(kl, config, row0, step):
         np.testing.assert_array_equal(f, frames[0])
 
 
+@pytest.mark.parametrize("case", ["monkey_c3_64_s4", "serre_96x54_s4", "proto_64_s4", "grid"])
+def test_sample_slices_render_identically(kl, case):
+    """slices K: a pixel's samples are K jobs handed out slice-major; the job of slice k continues the pixel
+    from the state the job of slice k - 1 published (on any lane, any XCD).  Every pixel's samples run in
+    order, so the frame is the one-pass frame and the oracle's, bit for bit, on both tree layouts (the grid
+    case: the 4-wide walk, slices on by default), whole frames and row tiles, both hand-out orders."""
+    import torch
+    from ensem3a_openclraytracer_amd import distributed as D
+    if case == "grid":
+        sc, cam, env, npix, spp, mb, ibl = W.CONFIGS["C5"].with_size(48, 27, 16).inputs()
+    else:
+        sc, cam, env, npix, _, mb, ibl = W.PARITY_CASES[case].inputs()
+        spp = 16
+    want = _oracle(sc, cam, env, npix, spp, mb, ibl)
+    w = int(cam[6])
+    try:
+        for width in (2, 4):
+            kl.native.set_option("bvh_width", width)
+            for k in (0, 2, 3, 5, 8):
+                kl.native.set_option("slices", k)
+                for h in (0, 1):
+                    kl.native.set_option("handout", h)
+                    np.testing.assert_array_equal(_launch(kl, sc, cam, env, npix, spp, mb, ibl, "fast"), want,
+                                                  err_msg=f"width {width} slices {k} handout {h}")
+                t = torch.zeros(3 * w * D.tile_rows(npix, w, 1, 3), dtype=torch.float32, device="cuda")
+                kl.native.render_device(cam, env, npix, spp, mb, 1, 3, t.data_ptr())
+                torch.cuda.synchronize()
+                np.testing.assert_array_equal(t.cpu().numpy(), want.reshape(-1, 3 * w)[1::3].ravel(),
+                                              err_msg=f"width {width} slices {k} tile 1::3")
+    finally:
+        kl.native.set_option("slices", -1)
+        kl.native.set_option("handout", -1)
+        kl.native.set_option("bvh_width", 0)
+    with pytest.raises(_native.NativeError, match="slices"):
+        kl.native.set_option("slices", 17)
+
+
 @pytest.mark.parametrize("case", ["cornell_128_s16", "monkey_c3_64_s4", "grid"])
 def test_block_handout_renders_identically(kl, case):
     """handout 1: each XCD group takes a contiguous block of the tile instead of interleaved chunks --
