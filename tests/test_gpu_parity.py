@@ -1209,6 +1209,7 @@ def test_sample_slices_render_identically(kl, case):
         spp = 16
     want = _oracle(sc, cam, env, npix, spp, mb, ibl)
     w = int(cam[6])
+    kl.native.set_option("pilot", 0)   # slices are for one-pass launches (the BVH2 walk's small frames take a pilot)
     try:
         for width in (2, 4):
             kl.native.set_option("bvh_width", width)
@@ -1227,6 +1228,7 @@ def test_sample_slices_render_identically(kl, case):
         kl.native.set_option("slices", -1)
         kl.native.set_option("handout", -1)
         kl.native.set_option("bvh_width", 0)
+        kl.native.set_option("pilot", -1)
     with pytest.raises(_native.NativeError, match="slices"):
         kl.native.set_option("slices", 17)
 
