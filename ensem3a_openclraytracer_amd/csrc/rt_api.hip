@@ -1168,9 +1168,11 @@ namespace {
 // resumable tree walk hand out each pixel's samples as K slices, slice-major, so that a tile ends on a
 // slice rather than on a whole pixel.  Auto: on the 4-wide walk (C5, whose pixels are all about equally
 // long: a tile of n pixels per resident lane ends after ceil(n) pixel times, 2.26 -> 3 on an eighth of
-// C5), K = kSlicesWide.  Sets fp's slice fields, sizes the device's state buffer and zeroes the
-// samples-done words on stream s (the launch's stream).
-constexpr int kSlicesWide = 4;
+// C5), K = kSlicesWide.  r05, C5 tiles rows 0::N (ms, K = off / 2 / 4 / 8): N=8 826 / 724 / 664 / 635,
+// N=4 1,395 / 1,273 / 1,221 / 1,197, N=2 2,536 / 2,409 / 2,361 / 2,343, N=1 4,796 / 4,692 / 4,642 / 4,648
+// (the wave cap of 6 instead: 838 / 1,444 / 2,651 / 5,066).  Sets fp's slice fields, sizes the device's
+// state buffer and zeroes the samples-done words on stream s (the launch's stream).
+constexpr int kSlicesWide = 8;
 hipError_t setup_slices(rt_ctx* ctx, Device& d, rt::FrameParams& fp, hipStream_t s) {
     fp.slices = 0;
     if (fp.pilot > 0 || fp.wf_buf || effective_traversal(ctx) != RT_TRAVERSAL_FAST || fp.nloc <= 0 ||
