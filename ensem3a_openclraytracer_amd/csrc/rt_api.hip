@@ -30,8 +30,6 @@
 // lanes still rendering: 36 on the BVH2 walk (C3 / C4 ms at 32 / 36 / 40: 138.8 / 136.8 / 136.5,
 // 446.8 / 452.6 / 455.0), 48 on the 4-wide walk (C5 at 40 / 48 / 52: 5,805 / 5,705 / 5,772)
 constexpr int kResumeMinBvh2 = 36, kResumeMinWide = 48;
-// wavefront trace phase: a refill of the idle lanes once this many are idle (option "wf_refill")
-constexpr int kWfRefillAuto = 16;
 #ifndef RT_BRUTE_MAX_DEFAULT
 #define RT_BRUTE_MAX_DEFAULT 64   // FAST tests every triangle of scenes up to this size (rt_set_option "brute_max")
 #endif
@@ -52,7 +50,6 @@ struct Device {
     DevBuf stack_ovf;             // FAST traversal stack entries beyond the LDS part
     DevBuf nodes, wnodes, wleaves, tri_fast, brute, brute_box, bvh9, tri_geo, tri_shade, tri_frame, mat, ibl, ibl_sum, out, out8, counts, work, scratch_a, scratch_b;
     DevBuf pilot;                 // two-pass launches: per-pixel state, cost and order (FrameParams::pilot_*)
-    DevBuf wf;                    // wavefront launches: the waves' path-state regions (FrameParams::wf_buf)
     DevBuf spec;                  // speculation: the trails' sample logs (FrameParams::spec_log)
     DevBuf slice;                 // sample slices: per-pixel state + samples done (FrameParams::slice_*)
     char* host_stage = nullptr;   // pinned staging for rt_render / rt_render_rgb8
@@ -114,9 +111,7 @@ struct rt_ctx {
     int pilot_chunk = 0;  // pixels ordered together (0 = auto: 64 brute force, 1 tree walk)
     int pilot_levels = 0; // cost bins of the order (0 = auto: 256)
     int stack_lds = 0;    // FAST stack entries per lane kept in LDS (0 = auto: rt::kStackLds, kStackLdsWide)
-    int wavefront = -1;   // tree walk split into trace / shade phases: path slots per lane (0 = off, -1 = auto)
     int ref_stack = 20;   // REF traversal stack capacity (20 = the reference's, stack.cl:4)
-    int wf_refill = 0;    // wavefront trace phase: idle lanes that trigger a refill (0 = auto)
     int spec = -1;        // small tiles: speculative trails per pixel in pass 2 (0 = off, 2, 4 or 8, -1 = auto)
     int handout = -1;     // pixel hand-out: 0 = interleaved chunks, 1 = a contiguous block per XCD group, -1 = auto
     int slices = -1;      // one-pass tree-walk launches: sample slices per pixel (FrameParams::slices; 0 off, -1 auto)
@@ -670,13 +665,6 @@ rt::DevScene dev_scene(const rt_ctx* ctx, const Device& d) {
     return s;
 }
 
-// option "wavefront" -1 (auto): path slots per lane of the wavefront walk, 0 = the per-lane megakernel
-int auto_wavefront(const rt_ctx* ctx, const rt::FrameParams& fp) {
-    (void)ctx;
-    (void)fp;
-    return 0;
-}
-
 int check_frame(rt_ctx* ctx, const float* cam, const float* env, int64_t npix, int spp, int row0, int row_step,
                 rt::FrameParams* fp) {
     if (!ctx) return set_err(nullptr, RT_ERR_ARG, "null context");
@@ -726,9 +714,6 @@ int check_frame(rt_ctx* ctx, const float* cam, const float* env, int64_t npix, i
     // 4,958 ms per frame; its L2-missing walk keeps neighbouring pixels on one XCD's L2), interleaved chunks
     // elsewhere (C3 / C4 -0.5 / +1 %, brute force untested)
     fp->handout = ctx->handout >= 0 ? ctx->handout : (use_wide(ctx) && effective_traversal(ctx) == RT_TRAVERSAL_FAST);
-    fp->wf_slots = ctx->wavefront > 0 ? ctx->wavefront : (ctx->wavefront < 0 ? auto_wavefront(ctx, *fp) : 0);
-    fp->wf_buf = nullptr;
-    fp->wf_refill = ctx->wf_refill > 0 ? ctx->wf_refill : kWfRefillAuto;
     fp->log_buf = nullptr;
     fp->log_cap = 0;
     fp->log_count = nullptr;
@@ -786,7 +771,7 @@ void rt_destroy(rt_ctx* ctx) {
         if (d.pending) (void)hipEventSynchronize(d.done);
         if (d.stream) (void)hipStreamSynchronize(d.stream);
         for (DevBuf* b : {&d.stack_ovf, &d.nodes, &d.wnodes, &d.wleaves, &d.tri_fast, &d.brute, &d.brute_box, &d.bvh9, &d.tri_geo, &d.tri_shade, &d.tri_frame, &d.mat, &d.ibl, &d.ibl_sum, &d.out,
-                          &d.out8, &d.counts, &d.work, &d.scratch_a, &d.scratch_b, &d.pilot, &d.wf, &d.spec, &d.slice})
+                          &d.out8, &d.counts, &d.work, &d.scratch_a, &d.scratch_b, &d.pilot, &d.spec, &d.slice})
             release(*b);
         if (d.host_stage) (void)hipHostFree(d.host_stage);
         if (d.stream) (void)hipStreamDestroy(d.stream);
@@ -928,16 +913,6 @@ int rt_set_option(rt_ctx* ctx, const char* key, int64_t value) {
         if (value != -1 && value != 0 && value != 2 && value != 4 && value != 8)
             return set_err(ctx, RT_ERR_ARG, "spec must be -1 (auto), 0 (off), 2, 4 or 8");
         ctx->spec = (int)value;
-        return RT_OK;
-    }
-    if (!std::strcmp(key, "wf_refill")) {
-        if (value < 0 || value > 64) return set_err(ctx, RT_ERR_ARG, "wf_refill must be 0 (auto) or 1..64");
-        ctx->wf_refill = (int)value;
-        return RT_OK;
-    }
-    if (!std::strcmp(key, "wavefront")) {
-        if (value < -1 || value > 16) return set_err(ctx, RT_ERR_ARG, "wavefront must be -1 (auto), 0 (off) or 1..16");
-        ctx->wavefront = (int)value;
         return RT_OK;
     }
     if (!std::strcmp(key, "block")) {
@@ -1097,7 +1072,7 @@ namespace {
 // or K), whose per-pixel costs order the rest of the frame, most expensive first (rt_kernels.hip
 // launch_render).  Sets fp's pilot fields and sizes the device's scratch for them.
 hipError_t setup_pilot(rt_ctx* ctx, Device& d, rt::FrameParams& fp) {
-    if (fp.wf_buf || ctx->pilot == 0 || effective_traversal(ctx) != RT_TRAVERSAL_FAST || fp.nloc <= 0) return hipSuccess;
+    if (ctx->pilot == 0 || effective_traversal(ctx) != RT_TRAVERSAL_FAST || fp.nloc <= 0) return hipSuccess;
     int k = ctx->pilot;
     if (k < 0) {   // auto: the tree walk on tiles of 1-16 pixels per resident lane (where the tail is long)
         const int64_t lanes = (int64_t)std::max(d.cus, 1) * rt::kWalkLanesPerCu;
@@ -1175,7 +1150,7 @@ namespace {
 constexpr int kSlicesWide = 8;
 hipError_t setup_slices(rt_ctx* ctx, Device& d, rt::FrameParams& fp, hipStream_t s) {
     fp.slices = 0;
-    if (fp.pilot > 0 || fp.wf_buf || effective_traversal(ctx) != RT_TRAVERSAL_FAST || fp.nloc <= 0 ||
+    if (fp.pilot > 0 || effective_traversal(ctx) != RT_TRAVERSAL_FAST || fp.nloc <= 0 ||
         ctx->hs.nbrute > 0 || fp.resume_min <= 0 || ctx->slices == 0)
         return hipSuccess;
     int k = ctx->slices > 0 ? ctx->slices : (use_wide(ctx) ? kSlicesWide : 1);
@@ -1195,28 +1170,6 @@ hipError_t setup_slices(rt_ctx* ctx, Device& d, rt::FrameParams& fp, hipStream_t
     return hipSuccess;
 }
 
-// Wavefront launches (FrameParams::wf_slots): size the device's path-state regions, or fall back to
-// the megakernel (wf_slots = 0) where the launch cannot take the wavefront walk
-hipError_t setup_wavefront(rt_ctx* ctx, Device& d, rt::FrameParams& fp) {
-    fp.wf_buf = nullptr;
-    if (fp.wf_slots <= 0 || effective_traversal(ctx) != RT_TRAVERSAL_FAST) {
-        fp.wf_slots = 0;
-        return hipSuccess;
-    }
-    const rt::DevScene ds = dev_scene(ctx, d);
-    if (!rt::wavefront_eligible(ds, fp)) {
-        fp.wf_slots = 0;
-        return hipSuccess;
-    }
-    const size_t need = rt::wavefront_bytes(ds, fp, ctx->block);
-    hipError_t e = hipSuccess;
-    // growing frees the old buffer from the host: the last launch (any stream) may still use it
-    if (d.wf.bytes < need && d.pending) e = hipEventSynchronize(d.done);
-    if (e == hipSuccess) e = ensure(d.wf, need);
-    if (e != hipSuccess) return e;
-    fp.wf_buf = (float*)d.wf.p;
-    return hipSuccess;
-}
 }  // namespace
 
 int rt_render_device(rt_ctx* ctx, int device_index, const float cam[10], const float env[5], int64_t npix, int spp,
@@ -1233,7 +1186,6 @@ int rt_render_device(rt_ctx* ctx, int device_index, const float cam[10], const f
     HIP_OR_RET(ctx, hipSetDevice(d.id));
     hipStream_t s = (hipStream_t)stream;  // NULL = the device's default (null) stream, HIP convention
     HIP_OR_RET(ctx, order_after_last(d, s));
-    HIP_OR_RET(ctx, setup_wavefront(ctx, d, fp));
     HIP_OR_RET(ctx, setup_pilot(ctx, d, fp));
     HIP_OR_RET(ctx, setup_slices(ctx, d, fp, s));
     HIP_OR_RET(ctx, rt::launch_render(dev_scene(ctx, d), fp, effective_traversal(ctx), ctx->block, d_out, nullptr,
@@ -1302,8 +1254,7 @@ int render_host(rt_ctx* ctx, const float cam[10], const float env[5], int64_t np
             d.host_stage_bytes = bytes;
         }
         HIP_OR_RET(ctx, order_after_last(d, d.stream));
-        HIP_OR_RET(ctx, setup_wavefront(ctx, d, fp));
-        HIP_OR_RET(ctx, setup_pilot(ctx, d, fp));
+            HIP_OR_RET(ctx, setup_pilot(ctx, d, fp));
         HIP_OR_RET(ctx, setup_slices(ctx, d, fp, d.stream));
         HIP_OR_RET(ctx, rt::launch_render(dev_scene(ctx, d), fp, effective_traversal(ctx), ctx->block,
                                           (float*)d.out.p, nullptr, (unsigned int*)d.work.p, d.stream));
@@ -1396,7 +1347,6 @@ int count_all(rt_ctx* ctx, const float cam[10], const float env[5], int64_t npix
     HIP_OR_RET(ctx, ensure(d.counts, sizeof h));
     HIP_OR_RET(ctx, hipMemsetAsync(d.counts.p, 0, sizeof h, d.stream));
     HIP_OR_RET(ctx, order_after_last(d, d.stream));
-    HIP_OR_RET(ctx, setup_wavefront(ctx, d, fp));
     HIP_OR_RET(ctx, rt::launch_render(dev_scene(ctx, d), fp, effective_traversal(ctx), ctx->block, (float*)d.out.p,
                                       (unsigned long long*)d.counts.p, (unsigned int*)d.work.p, d.stream));
     HIP_OR_RET(ctx, mark_launch(d, d.stream));

@@ -1,5 +1,5 @@
-// Device code shared by the render kernels (rt_kernels.hip: the per-lane megakernels; rt_wavefront.hip:
-// the wavefront kernel): traversals, shading arithmetic, launch constants, pixel hand-out.  Included by
+// Device code shared by the render kernels (rt_kernels.hip: the per-lane megakernels; rt_spec.hip: the
+// speculative-trail kernel): traversals, shading arithmetic, launch constants, pixel hand-out.  Included by
 // the .hip translation units only; everything is internal to each of them (anonymous namespace).
 //
 // Numerics: every OpenCL builtin of the reference is taken from rtm.h and the including file is
@@ -557,8 +557,8 @@ struct LaunchConst {
     float pas;                        // 1.0 / cam[6]
 };
 
-// evaluated once per launch: on the device (make_const_kernel) or on the host (the wavefront launch passes
-// it by value); rtm.h makes both bit-identical
+// evaluated once per launch on the device (make_const_kernel); rtm.h makes it bit-identical to a host
+// evaluation
 __host__ __device__ inline LaunchConst make_const(const FrameParams& F) {
     LaunchConst c;
     const float* cam = F.cam;

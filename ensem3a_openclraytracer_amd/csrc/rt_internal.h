@@ -151,12 +151,6 @@ struct FrameParams {
     float4* slice_state;
     uint32_t* slice_ready;
     const uint32_t* pilot_order;
-    // Wavefront launches (rt_wavefront.hip, option "wavefront"): the tree walk split into a trace phase
-    // and a shade phase per wave, every path's state in HBM between them.  wf_slots = path slots per
-    // lane (0: the per-lane megakernel); wf_buf: the per-wave regions (wavefront_bytes)
-    int32_t wf_slots;
-    float* wf_buf;
-    int32_t wf_refill;   // trace phase: idle lanes that trigger a refill from the wave's ray queue (1..64)
     // debug event log of one pixel (rt_debug_pixel_log only; unused by the product launches)
     int64_t log_pixel;
     float* log_buf;
@@ -174,12 +168,6 @@ hipError_t launch_prep_frames(const DevScene& sc, float4* frame, hipStream_t str
 hipError_t launch_ibl_sum(const uchar4* rgba, int w, int h, uint32_t* sum, hipStream_t stream);
 hipError_t launch_gamma(const float* d_in, float* d_out, int64_t n, hipStream_t stream);
 hipError_t launch_rgb8(const float* d_in, uint8_t* d_out, int64_t n, bool gamma, hipStream_t stream);
-// Wavefront tree walk (rt_wavefront.hip): whether a launch takes it, the bytes of fp.wf_buf it needs,
-// and the launch (called by launch_render when fp.wf_slots > 0)
-bool wavefront_eligible(const DevScene& sc, const FrameParams& fp);
-size_t wavefront_bytes(const DevScene& sc, const FrameParams& fp, int block);
-hipError_t launch_wavefront(const DevScene& sc, const FrameParams& fp, int block, float* d_out,
-                            unsigned long long* d_counts, unsigned int* d_work, hipStream_t stream);
 // Sample-parallel speculation (rt_spec.hip): pass 2 of a pilot launch of the BVH2 walk with fp.spec
 // trails per pixel; spec_log_bytes = the size of fp.spec_log it needs on a device of `cus` CUs (one log
 // per resident lane, launch_spec keeps the grid within them); at most kSpecTrails trails per pixel;

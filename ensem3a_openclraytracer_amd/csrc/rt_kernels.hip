@@ -1077,8 +1077,6 @@ hipError_t launch_resume(const DevScene& sc, const FrameParams& fp, int block, f
 template <bool COUNT>
 hipError_t launch_fast(const DevScene& sc, const FrameParams& fp, int block, float* d_out,
                        unsigned long long* d_counts, unsigned int* d_work, hipStream_t stream) {
-    if (fp.wf_buf && wavefront_eligible(sc, fp))   // shading split from traversal (rt_wavefront.hip)
-        return launch_wavefront(sc, fp, block, d_out, d_counts, d_work, stream);
     const size_t scene_bytes = (size_t)(kNodeF4 * sc.nnodes + 3 * sc.ntri) * sizeof(float4);
     const bool smem = sc.ntri > 0 && sc.nbrute == 0 && scene_bytes <= kLdsSceneMax;
     const bool ovf = sc.nbrute == 0 && sc.stack_lds < sc.depth;

@@ -89,14 +89,14 @@ int rt_set_env(rt_ctx* ctx, const uint8_t* rgba, int w, int h);
  * same hits), "spec" (second pass of a pilot launch of the BVH2 walk: 2/4/8
  * speculative trails per pixel from guessed RNG offsets, stitched in chain
  * order, 0 = off, -1 = auto: chosen on the device on small tiles -- same
- * frame), "wavefront" (tree walk split into trace / shade phases per wave with
- * K path slots per lane in HBM, 0 = the per-lane kernel, -1 = auto = 0 --
+ * frame), "slices" (one-pass tree-walk launches: each pixel's samples as K
+ * jobs handed out slice-major, 0 = off, -1 = auto: 8 on the 4-wide walk --
  * same frame), "handout" (1 = a contiguous pixel block per XCD group, 0 =
  * interleaved chunks, -1 = auto: 1 on the 4-wide walk), "waves" (persistent
  * grid: at most this many waves per SIMD, 0 = occupancy limit), "block"
  * (threads per block: 64, 128 or 256), and the tuning switches documented in
  * DESIGN.md 4.2 ("sun_skip", "sun_any", "fixed_point", "sun_cache", "pilot",
- * "pilot_chunk", "pilot_levels", "stack_lds", "ref_stack", "wf_refill",
+ * "pilot_chunk", "pilot_levels", "stack_lds", "ref_stack",
  * "bvh_width"): every option renders the same frame except "ref_stack" (REF's
  * stack slots; 20 = the reference's, more = no silent drops).
  * "bvh" and "brute_max" may be changed after rt_set_scene. */

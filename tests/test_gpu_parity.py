@@ -1082,44 +1082,6 @@ def test_two_pass_pilot_full_frame(kl, config, pilot, spp):
     np.testing.assert_array_equal(out[pilot], out[0])
 
 
-@pytest.mark.parametrize("case", ["monkey_c3_64_s4", "serre_96x54_s4", "proto_64_s4", "furnace_64_s4", "grid"])
-def test_wavefront_renders_identically(kl, case):
-    """wavefront K: each persistent wave keeps 64 K paths in HBM and alternates a shade phase (naiveGI's
-    logic for every path, new pixels, the live paths compacted into the wave's ray queue) with a trace
-    phase (lanes take queued rays as soon as theirs is done).  One ray in flight per pixel and the
-    megakernel's shading order: the frame and every work counter are the megakernel's, bit for bit,
-    on both tree layouts (BVH2 with the glass prefix; 4-wide, the grid case spilling its stack to HBM)."""
-    if case == "grid":
-        sc, cam, env, npix, spp, mb, ibl = W.CONFIGS["C5"].with_size(48, 27, 2).inputs()
-    else:
-        sc, cam, env, npix, spp, mb, ibl = W.PARITY_CASES[case].inputs()
-    want = _oracle(sc, cam, env, npix, spp, mb, ibl)
-    kl.native.set_option("brute_max", 0)   # the tree walk, also for small scenes
-    kl.native.set_option("walk_team", 1)   # node counts compared with the one-lane walk (teams steal)
-    try:
-        for width in (2, 4):
-            kl.native.set_option("bvh_width", width)
-            kl.native.set_option("wavefront", 0)
-            base = _launch(kl, sc, cam, env, npix, spp, mb, ibl, "fast")
-            c0 = kl.native.count_work_detail(cam, env, npix, spp, mb)
-            for k in (1, 2, 3, 4, 8):
-                kl.native.set_option("wavefront", k)
-                got = _launch(kl, sc, cam, env, npix, spp, mb, ibl, "fast")
-                np.testing.assert_array_equal(got, base, err_msg=f"width {width} K {k}")
-                ck = kl.native.count_work_detail(cam, env, npix, spp, mb)
-                for key in ("rays", "samples", "ev_diffuse", "ev_glossy", "ev_glass", "sun_terms", "env_lookups",
-                            "node_fetches", "tri_tests", "box_tests"):
-                    assert ck[key] == c0[key], (width, k, key, ck[key], c0[key])
-            np.testing.assert_array_equal(base, want)
-    finally:
-        kl.native.set_option("wavefront", -1)
-        kl.native.set_option("walk_team", 0)
-        kl.native.set_option("bvh_width", 0)
-        kl.native.set_option("brute_max", 64)
-    with pytest.raises(_native.NativeError, match="wavefront"):
-        kl.native.set_option("wavefront", 17)
-
-
 def test_team_walk_steals_across_the_lds_cap(kl):
     """Team walk on a deep BVH2 (grid, 23 levels) with only 8 stack entries per lane in LDS: a thief's
     steal of a teammate's bottom entry reaches into the HBM overflow part once 8 entries were stolen
@@ -1237,21 +1199,18 @@ def test_sample_slices_render_identically(kl, case):
 def test_block_handout_renders_identically(kl, case):
     """handout 1: each XCD group takes a contiguous block of the tile instead of interleaved chunks --
     a different assignment of pixels to waves, never a different frame (lock-step brute force, BVH2
-    walk, 4-wide walk and the wavefront walk)."""
+    walk and 4-wide walk)."""
     if case == "grid":
         sc, cam, env, npix, spp, mb, ibl = W.CONFIGS["C5"].with_size(48, 27, 2).inputs()
     else:
         sc, cam, env, npix, spp, mb, ibl = W.PARITY_CASES[case].inputs()
     want = _oracle(sc, cam, env, npix, spp, mb, ibl)
     try:
-        for wf in (0, 4):
-            kl.native.set_option("wavefront", wf)
-            for h in (0, 1):
-                kl.native.set_option("handout", h)
-                np.testing.assert_array_equal(_launch(kl, sc, cam, env, npix, spp, mb, ibl, "fast"), want,
-                                              err_msg=f"wavefront {wf} handout {h}")
+        for h in (0, 1):
+            kl.native.set_option("handout", h)
+            np.testing.assert_array_equal(_launch(kl, sc, cam, env, npix, spp, mb, ibl, "fast"), want,
+                                          err_msg=f"handout {h}")
     finally:
         kl.native.set_option("handout", -1)
-        kl.native.set_option("wavefront", -1)
     with pytest.raises(_native.NativeError, match="handout"):
         kl.native.set_option("handout", 2)

@@ -101,48 +101,3 @@ def test_wide_quantisation_reports_failure(lo, hi):
     p = np.float32(np.nanmin(np.asarray(lo, np.float32)))
     e, _, _ = _quantise(p, lo, hi)
     assert e == -1
-
-
-def _code_object_notes(tmp_path):
-    llvm = "/opt/rocm/lib/llvm/bin"
-    if not os.path.exists(os.path.join(llvm, "llvm-readelf")):
-        pytest.skip("ROCm LLVM tools absent")
-    import subprocess
-    fat, co = str(tmp_path / "fat.bin"), str(tmp_path / "k.co")
-    subprocess.run([f"{llvm}/llvm-objcopy", f"--dump-section=.hip_fatbin={fat}", LIB, str(tmp_path / "x.so")],
-                   check=True)
-    # the library's fat binary holds one offload bundle per translation unit
-    blob = open(fat, "rb").read()
-    magic = b"__CLANG_OFFLOAD_BUNDLE__"
-    starts = [m.start() for m in re.finditer(re.escape(magic), blob)] + [len(blob)]
-    notes = ""
-    for i, (a, b) in enumerate(zip(starts, starts[1:])):
-        part = str(tmp_path / f"b{i}.bin")
-        with open(part, "wb") as f:
-            f.write(blob[a:b])
-        subprocess.run([f"{llvm}/clang-offload-bundler", "--unbundle", "--type=o", f"--input={part}",
-                        "--targets=hipv4-amdgcn-amd-amdhsa--gfx950", f"--output={co}"], check=True)
-        notes += subprocess.run([f"{llvm}/llvm-readelf", "--notes", co], capture_output=True, text=True,
-                                check=True).stdout
-    return notes
-
-
-def test_wavefront_kernel_arguments_match_the_struct_it_rereads(tmp_path):
-    """The wavefront kernel re-reads (scene, frame, launch constants) from its kernel-argument segment
-    as one struct (rt_wavefront.hip WfArgs, RT_WF_OPAQUE): the code object's argument metadata must place
-    the three by-value arguments back to back at their natural alignment, which WfArgs' static_asserts
-    assume."""
-    notes = _code_object_notes(tmp_path)
-    kernels = notes.split("- .agpr_count:")   # one metadata map per kernel, keys in order: .args ... .name
-    found = 0
-    for k in kernels:
-        m = re.search(r"\.name:\s+(\S+)", k)
-        if not m or "wave_kernel" not in m.group(1):
-            continue
-        args = re.findall(r"\.offset:\s+(\d+)\s+\.size:\s+(\d+)\s+\.value_kind:\s+(\w+)", k)
-        byval = [(int(o), int(s)) for o, s, kind in args if kind == "by_value"][:3]
-        assert len(byval) == 3, args[:4]
-        (o0, s0), (o1, s1), (o2, _) = byval
-        assert o0 == 0 and o1 == (s0 + 7) // 8 * 8 and o2 == (o1 + s1 + 3) // 4 * 4, byval
-        found += 1
-    assert found >= 8   # COUNT x OVF x WIDE instantiations

@@ -13,7 +13,7 @@ import time
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
-DEFAULTS = {"spec": -1, "wavefront": -1, "wf_refill": 0, "team": 0, "sun_cache": 1, "walk_team": 0, "brute_max": 64, "waves": 0, "block": 128, "fixed_point": 1, "pilot": -1, "pilot_chunk": 0, "pilot_levels": 0, "stack_lds": 0, "step": 0, "resume_min": -1, "bvh_width": 0}
+DEFAULTS = {"spec": -1, "slices": -1, "team": 0, "sun_cache": 1, "walk_team": 0, "brute_max": 64, "waves": 0, "block": 128, "fixed_point": 1, "pilot": -1, "pilot_chunk": 0, "pilot_levels": 0, "stack_lds": 0, "step": 0, "resume_min": -1, "bvh_width": 0}
 
 
 def main():

@@ -2,7 +2,7 @@
 
     python tools/summarize_profiles.py gpurun_out/SESSION:CFG[:OPTS] TAG WORKLOAD [FRAMES]
         the kt / pmc steps of tools/gpu_session.py (gpurun_out/SESSION_kt_CFG[_OPTS],
-        SESSION_pmc_CFG_GROUP[_OPTS]; OPTS = the step's option suffix, e.g. wavefront-16)
+        SESSION_pmc_CFG_GROUP[_OPTS]; OPTS = the step's option suffix, e.g. slices-8)
     python tools/summarize_profiles.py DIR TAG WORKLOAD [FRAMES]
         DIR/kt, DIR/fetch, DIR/write, DIR/req, DIR/sq, DIR/hit (one pass each)
     --wave-stats FILE:CONFIG  also record the SIMD efficiency of the render loop (tools/wave_stats.py's
@@ -38,7 +38,7 @@ import sys
 import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-# FAST, uninstrumented (any variant): the megakernels and the wavefront kernel
+# FAST, uninstrumented (any variant): the megakernels
 KERNEL = r"render(_resume)?_kernel<(0, )?false, false|wave_kernel<false"
 GROUPS = ("fetch", "write", "dram", "req", "sq", "hit")
 

@@ -14,7 +14,7 @@ from ensem3a_openclraytracer_amd import _native  # noqa: E402
 from ensem3a_openclraytracer_amd import workloads as W  # noqa: E402
 
 # rt_set_option defaults of the options a set may change (rt_api.hip)
-DEFAULTS = {"spec": -1, "wavefront": -1, "pilot": -1, "resume_min": -1, "handout": -1, "bvh_width": 0, "brute_max": 64,
+DEFAULTS = {"spec": -1, "slices": -1, "pilot": -1, "resume_min": -1, "handout": -1, "bvh_width": 0, "brute_max": 64,
             "block": 128, "fixed_point": 1, "sun_cache": 1}
 names = (sys.argv[1] if len(sys.argv) > 1 else "C3").split(",")
 sets = [dict(kv.split("=") for kv in filter(None, spec.split(",")))
