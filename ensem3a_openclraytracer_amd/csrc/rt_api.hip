@@ -1067,6 +1067,14 @@ int64_t rt_tile_rows(int64_t npix, int width, int row0, int row_step) {
 }
 
 namespace {
+// Sample slices per pixel (setup_slices): auto on the 4-wide walk, and on BVH2 tiles of at least
+// kSlicesMinPerLane pixels per resident lane, where they replace the two-pass pilot.  r05 (ms, pilot auto
+// vs slices 8 with the pilot off; rows 0::N): C3 N=1 126.5 / 114.8, N=2 78.7 / 65.6, N=4 54.3 / 84.8
+// (teams + trails); C4 N=1 303.6 / 284.8, N=2 181.5 / 254.9 (3/4 of C4's pixels are sky, finished by
+// the pilot pass: the rest is one pixel per lane, where trails win), N=4 121.4 / 318.4
+constexpr int kSlicesWide = 8;
+constexpr int64_t kSlicesMinPerLane = 4;
+
 // Two-pass launches (FrameParams::pass): FAST tree-walk renders of tiles with more pixels than the
 // device keeps lanes resident get a pilot pass of spp / 8 samples (option "pilot": -1 auto, 0 off,
 // or K), whose per-pixel costs order the rest of the frame, most expensive first (rt_kernels.hip
@@ -1080,6 +1088,8 @@ hipError_t setup_pilot(rt_ctx* ctx, Device& d, rt::FrameParams& fp) {
         // when they are reordered: r03 row tiles 1/2, 1/4, 1/8: 3,005 / 1,626 / 937 ms without the pilot,
         // 3,185 / 1,694 / 938 with it
         if (ctx->hs.nbrute > 0 || use_wide(ctx) || fp.spp < 16 || fp.nloc > 16 * lanes) return hipSuccess;
+        // tiles of kSlicesMinPerLane or more pixels per resident lane take sample slices instead (setup_slices)
+        if (ctx->slices != 0 && fp.nloc >= kSlicesMinPerLane * lanes) return hipSuccess;
         // spp/8 samples, small tiles (multi-GPU row tiles, whose pass 2 takes teams or speculative trails)
         // included: r04 1/8 tiles with trails, pilot spp/16 / spp/8 / 3spp/16: C4 80.8 / 78.3 / 77.0 ms,
         // C3 35.3 / 33.9 / 35.1 ms; 1/4 tiles C4 120.7 / 119.9 / 129.1, C3 54.8 / 54.8 / 56.1 (r03, teams
@@ -1147,13 +1157,14 @@ namespace {
 // N=4 1,395 / 1,273 / 1,221 / 1,197, N=2 2,536 / 2,409 / 2,361 / 2,343, N=1 4,796 / 4,692 / 4,642 / 4,648
 // (the wave cap of 6 instead: 838 / 1,444 / 2,651 / 5,066).  Sets fp's slice fields, sizes the device's
 // state buffer and zeroes the samples-done words on stream s (the launch's stream).
-constexpr int kSlicesWide = 8;
 hipError_t setup_slices(rt_ctx* ctx, Device& d, rt::FrameParams& fp, hipStream_t s) {
     fp.slices = 0;
     if (fp.pilot > 0 || effective_traversal(ctx) != RT_TRAVERSAL_FAST || fp.nloc <= 0 ||
         ctx->hs.nbrute > 0 || fp.resume_min <= 0 || ctx->slices == 0)
         return hipSuccess;
-    int k = ctx->slices > 0 ? ctx->slices : (use_wide(ctx) ? kSlicesWide : 1);
+    const int64_t lanes = (int64_t)std::max(d.cus, 1) * rt::kWalkLanesPerCu;
+    int k = ctx->slices > 0 ? ctx->slices
+                            : (use_wide(ctx) || fp.nloc >= kSlicesMinPerLane * lanes) ? kSlicesWide : 1;
     k = std::min(k, fp.spp / 2);   // every slice at least two samples
     if (k <= 1 || (int64_t)fp.nloc * k >= ((int64_t)1 << 32)) return hipSuccess;
     const size_t n = (size_t)fp.nloc;

@@ -12,6 +12,8 @@ dispatch of a frame) of gpurun_out/SESSION_pmc_CFG_GROUP[_OPTS]/ are summed and 
   wait_frac              SQ_WAIT_ANY / SQ_WAVE_CYCLES: wave-cycles waiting on a counter
   ta_busy_frac           TA_TA_BUSY_sum / (32 x GRBM_GUI_ACTIVE) (the normalisation of the r03 summaries)
   vmem_rd_per_frame      SQ_INSTS_VMEM_RD (wave-level vector-memory read instructions)
+  stall                  (the stall pass) wave-cycles issuing / parked on a counter / ready but not issued
+                         (SQ_ACTIVE_INST_ANY, SQ_WAIT_ANY, SQ_WAIT_INST_ANY over SQ_WAVE_CYCLES: disjoint)
 """
 import csv
 import glob
@@ -53,7 +55,21 @@ def main():
             row = {}
             sq, t, nd = sums(os.path.join(ROOT, "gpurun_out", f"{sess}_pmc_{c}_sq{suf}"))
             ta, _, _ = sums(os.path.join(ROOT, "gpurun_out", f"{sess}_pmc_{c}_ta{suf}"))
+            stall, t2, nd2 = sums(os.path.join(ROOT, "gpurun_out", f"{sess}_pmc_{c}_stall{suf}"))
+            if stall:
+                wc = stall["SQ_WAVE_CYCLES"]
+                row["stall"] = {
+                    "kernel_ms": round(t2 / frames * 1e3, 3),
+                    "active_frac": round(stall["SQ_ACTIVE_INST_ANY"] / wc, 4),     # wave-cycles issuing
+                    "wait_frac": round(stall["SQ_WAIT_ANY"] / wc, 4),              # parked in s_waitcnt / barrier
+                    "wait_inst_frac": round(stall["SQ_WAIT_INST_ANY"] / wc, 4),    # ready but not issued (pipe / dependency)
+                    "wait_inst_lds_frac": round(stall["SQ_WAIT_INST_LDS"] / wc, 4),
+                    "valu_issue_frac": round(stall["SQ_INSTS_VALU"] * 64 / t2 / PEAK, 4),
+                    "per_frame": {k: stall[k] / frames for k in ("SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_LDS")},
+                }
             if not sq:
+                if stall:
+                    res["rows"][f"{name} {c}"] = row
                 continue
             row["dispatches"] = nd
             row["kernel_ms"] = round(t / frames * 1e3, 3)

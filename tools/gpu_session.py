@@ -18,7 +18,7 @@ STEP forms (values after '=' separated by ':'):
   tiles=CFG:NS[:SETS]           tools/occupancy_probe.py CFG NS "SETS" (SETS: k=v,k=v;k=v)
   kt=CFG[:OPTS[:STEPS]]         rocprofv3 --kernel-trace --stats of bench.py (STEPS steps, default 1, after 1
                                 warmup) -> gpurun_out/TAG_kt_CFG
-  pmc=CFG:GROUP[:OPTS[:STEPS]]  one rocprofv3 --pmc pass (GROUP: fetch, write, req, sq, hit, ta) of bench.py
+  pmc=CFG:GROUP[:OPTS[:STEPS]]  one rocprofv3 --pmc pass (GROUP: fetch, write, req, sq, hit, ta, stall) of bench.py
   py=SCRIPT[:ARGS]              python3 -u SCRIPT ARGS (ARGS split on '+')
   ktpy=NAME:SCRIPT[:ARGS]       rocprofv3 --kernel-trace --stats of a py step -> gpurun_out/TAG_kt_NAME
 Limits: LIMIT_<KIND> env overrides the default seconds of a step kind.
@@ -38,6 +38,8 @@ PMC = {
     "write": "WRITE_SIZE",
     "hit": "TCC_HIT_sum TCC_MISS_sum TCC_REQ_sum TCC_EA0_WRREQ_64B_sum",
     "req": "TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_128B_sum",
+    "stall": "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_WAIT_INST_LDS SQ_ACTIVE_INST_ANY SQ_INSTS_SALU SQ_INSTS_LDS "
+             "SQ_INSTS_VALU GRBM_GUI_ACTIVE",
     "ta": "TA_TA_BUSY_sum SQ_INSTS_VMEM_RD SQ_INSTS_VALU SQ_WAVE_CYCLES GRBM_GUI_ACTIVE",
     "sq": "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_THREAD_CYCLES_VALU "
           "SQ_WAIT_ANY SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE GRBM_COUNT",
