@@ -1159,13 +1159,15 @@ namespace {
 // state buffer and zeroes the samples-done words on stream s (the launch's stream).
 hipError_t setup_slices(rt_ctx* ctx, Device& d, rt::FrameParams& fp, hipStream_t s) {
     fp.slices = 0;
-    if (fp.pilot > 0 || effective_traversal(ctx) != RT_TRAVERSAL_FAST || fp.nloc <= 0 ||
-        ctx->hs.nbrute > 0 || fp.resume_min <= 0 || ctx->slices == 0)
+    if (effective_traversal(ctx) != RT_TRAVERSAL_FAST || fp.nloc <= 0 || ctx->hs.nbrute > 0 || fp.resume_min <= 0 ||
+        ctx->slices == 0)
         return hipSuccess;
     const int64_t lanes = (int64_t)std::max(d.cus, 1) * rt::kWalkLanesPerCu;
+    // pilot launches: pass 2 slices the samples after the pilot's when the device gives it one lane per pixel
+    // (pilot_team_pick_kernel: more unfinished pixels than lanes); the team and trail kernels take none
     int k = ctx->slices > 0 ? ctx->slices
-                            : (use_wide(ctx) || fp.nloc >= kSlicesMinPerLane * lanes) ? kSlicesWide : 1;
-    k = std::min(k, fp.spp / 2);   // every slice at least two samples
+                            : (use_wide(ctx) || fp.pilot > 0 || fp.nloc >= kSlicesMinPerLane * lanes) ? kSlicesWide : 1;
+    k = std::min(k, (fp.spp - std::max(fp.pilot, 0)) / 2);   // every slice at least two samples
     if (k <= 1 || (int64_t)fp.nloc * k >= ((int64_t)1 << 32)) return hipSuccess;
     const size_t n = (size_t)fp.nloc;
     const size_t need = n * 32 + n * sizeof(uint32_t);

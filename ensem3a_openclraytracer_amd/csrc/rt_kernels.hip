@@ -441,7 +441,11 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WIDE ?
     int ndraw = 0;       // pass 1, BVH2 walk: random numbers the pixel drew (its RNG offset, pilot_draws)
     // sample slices (FrameParams::slices): the sample count this job stops at; while the job waits for the
     // slice before it (phase WAIT_SLICE), the job's slice index
-    const unsigned nsl = (TS == 1 && F.slices > 1 && F.pass == 0) ? (unsigned)F.slices : 1u;
+    // (one-pass launches, and pass 2 of a pilot launch: the samples after the pilot's sb = F.pilot; slice k
+    // of a pixel ends at sb + (k + 1) (spp - sb) / nsl)
+    const unsigned nsl = (TS == 1 && F.slices > 1 && F.pass != 1) ? (unsigned)F.slices : 1u;
+    const int sb = F.pass == 2 ? F.pilot : 0;
+    auto slice_end = [&](unsigned k) { return sb + (int)((k + 1u) * (unsigned)(spp - sb) / nsl); };
     int lim = spp;
     // The deterministic prefix of the pixel's samples (FrameParams::fixed_point; BVH2 walk): a sample's
     // path up to its first diffuse or glossy bounce draws no random number -- it is the cached camera
@@ -566,7 +570,10 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WIDE ?
                     sun_c = SUN_UNKNOWN;
                     phase = PRIMARY;
                     logme = LOG && i == F.log_pixel;
-                    if (F.pass == 2) {   // continue from the pilot state: camera hit cached, sample s next
+                    if (sl > 0) {
+                        lim = (int)sl;   // continues the pixel once slice sl - 1 is done (below)
+                        phase = WAIT_SLICE;
+                    } else if (F.pass == 2) {   // continue from the pilot state: camera hit cached, sample s next
                         const float4 a = F.pilot_state[2 * (int64_t)p], b = F.pilot_state[2 * (int64_t)p + 1];
                         acc = rtm_v3(a.x, a.y, a.z);
                         kc = a.w;
@@ -577,12 +584,11 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WIDE ?
                         tri = tc; j = 0;
                         so = rtm_v3(1, 1, 1);
                         drew = false;
+                        lim = slice_end(0);
                         phase = s >= spp ? FETCH : PREP;   // finished in pass 1: already written
-                    } else if (sl > 0) {
-                        lim = (int)sl;   // continues the pixel once slice sl - 1 is done (below)
-                        phase = WAIT_SLICE;
+                        if (nsl > 1 && s >= spp) save_slice();   // ... and its later slices have nothing to do
                     } else {
-                        lim = (int)(((unsigned)spp) / nsl);
+                        lim = slice_end(0);
                         start(C.position, cd);
                     }
                 } else {
@@ -594,7 +600,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WIDE ?
         if (nsl > 1 && phase == WAIT_SLICE) {
             // slices: the previous slice's samples done, published by the lane that ran it (save_slice); its
             // state is read with sc1 loads (past this CU's L1) once the count is there
-            const unsigned need_s = (unsigned)(lim * spp) / nsl;
+            const unsigned need_s = (unsigned)slice_end((unsigned)lim - 1u);
             const unsigned done_s = __hip_atomic_load((gu32*)(F.slice_ready + p), __ATOMIC_RELAXED,
                                                       __HIP_MEMORY_SCOPE_AGENT);
             if (done_s >= need_s) {
@@ -613,7 +619,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WIDE ?
                 tri = tc; j = 0;
                 so = rtm_v3(1, 1, 1);
                 drew = false;
-                lim = (int)((unsigned)(lim + 1) * (unsigned)spp / nsl);
+                lim = slice_end((unsigned)lim);
                 phase = s >= spp ? FETCH : PREP;   // finished early (a sample that draws nothing): written
             }
         }

@@ -1197,6 +1197,31 @@ def test_sample_slices_render_identically(kl, case):
         kl.native.set_option("slices", 17)
 
 
+@pytest.mark.parametrize("case", ["monkey_c3_64_s4", "serre_96x54_s4", "proto_64_s4"])
+def test_pilot_pass2_slices_render_identically(kl, case):
+    """Pass 2 of a pilot launch with one lane per pixel continues each pixel's remaining samples as K slices
+    (pixels in pilot-cost order, slice-major); pixels the pilot pass finished publish their state at once.
+    Bit for bit the one-pass frame and the oracle's, for several pilot lengths and K, and auto."""
+    sc, cam, env, npix, _, mb, ibl = W.PARITY_CASES[case].inputs()
+    spp = 24
+    want = _oracle(sc, cam, env, npix, spp, mb, ibl)
+    kl.native.set_option("brute_max", 0)
+    kl.native.set_option("bvh_width", 2)
+    kl.native.set_option("walk_team", 1)   # one lane per pixel in pass 2 (the auto pick may take teams)
+    kl.native.set_option("spec", 0)
+    try:
+        for pilot in (2, 5):
+            kl.native.set_option("pilot", pilot)
+            for k in (0, 2, 3, 8, -1):
+                kl.native.set_option("slices", k)
+                np.testing.assert_array_equal(_launch(kl, sc, cam, env, npix, spp, mb, ibl, "fast"), want,
+                                              err_msg=f"pilot {pilot} slices {k}")
+    finally:
+        for key, v in (("slices", -1), ("pilot", -1), ("spec", -1), ("walk_team", 0), ("bvh_width", 0),
+                       ("brute_max", 64)):
+            kl.native.set_option(key, v)
+
+
 @pytest.mark.parametrize("case", ["cornell_128_s16", "monkey_c3_64_s4", "grid"])
 def test_block_handout_renders_identically(kl, case):
     """handout 1: each XCD group takes a contiguous block of the tile instead of interleaved chunks --
