@@ -472,6 +472,11 @@ __device__ Hit trace_brute_compact(const DevScene& S, rtm_f3 o, rtm_f3 d, char* 
         // to back, then the passes are queued (culling uses the best hit as of the group's start:
         // conservative)
         const ConstF4 cb = as_const(S.brute_box);
+#ifdef RT_BRUTE_FMA
+        // variant: (b - o) / d as fma(b, 1/d, -o/d), one rounding of the loop-invariant -o/d per ray (A/B only:
+        // a different rounding at box faces than the tree walk's slab)
+        const float nox = -o.x * ix, noy = -o.y * iy, noz = -o.z * iz;
+#endif
         for (int g0 = 0; g0 < S.nbox; g0 += kBoxGroup) {
             float4 bx[2 * kBoxGroup];
 #pragma unroll
@@ -481,8 +486,16 @@ __device__ Hit trace_brute_compact(const DevScene& S, rtm_f3 o, rtm_f3 d, char* 
 #pragma unroll
             for (int j = 0; j < kBoxGroup; ++j) {
                 float tn, tx;
+#ifdef RT_BRUTE_FMA
+                const float x0 = fmaf(bx[2 * j].x, ix, nox), x1 = fmaf(bx[2 * j].y, ix, nox);
+                const float y0 = fmaf(bx[2 * j].z, iy, noy), y1 = fmaf(bx[2 * j].w, iy, noy);
+                const float z0 = fmaf(bx[2 * j + 1].x, iz, noz), z1 = fmaf(bx[2 * j + 1].y, iz, noz);
+                tn = fmaxf(fmaxf(fminf(x0, x1), fminf(y0, y1)), fminf(z0, z1));
+                tx = fminf(fminf(fmaxf(x0, x1), fmaxf(y0, y1)), fmaxf(z0, z1));
+#else
                 slab(bx[2 * j].x, bx[2 * j].y, bx[2 * j].z, bx[2 * j].w, bx[2 * j + 1].x, bx[2 * j + 1].y, o, ix, iy,
                      iz, tn, tx);
+#endif
                 pass[j] = box_hit(tn, tx, cull);
             }
 #pragma unroll
