@@ -1080,7 +1080,8 @@ constexpr int64_t kSlicesMinPerLane = 4;
 // or K), whose per-pixel costs order the rest of the frame, most expensive first (rt_kernels.hip
 // launch_render).  Sets fp's pilot fields and sizes the device's scratch for them.
 hipError_t setup_pilot(rt_ctx* ctx, Device& d, rt::FrameParams& fp) {
-    if (ctx->pilot == 0 || effective_traversal(ctx) != RT_TRAVERSAL_FAST || fp.nloc <= 0) return hipSuccess;
+    if (ctx->pilot == 0 || effective_traversal(ctx) != RT_TRAVERSAL_FAST || fp.nloc <= 0 || use_wide(ctx))
+        return hipSuccess;   // (the 4-wide walk is one-pass: its pilot measured slower, r02-r03)
     int k = ctx->pilot;
     if (k < 0) {   // auto: the tree walk on tiles of 1-16 pixels per resident lane (where the tail is long)
         const int64_t lanes = (int64_t)std::max(d.cus, 1) * rt::kWalkLanesPerCu;

@@ -383,6 +383,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WIDE ?
     if (F.walk_team_dev && __builtin_amdgcn_readfirstlane(*F.walk_team_dev) != TS) return;
     extern __shared__ int lds_stack[];
     const int B = blockDim.x;
+    // two-pass launches are BVH2-only (the 4-wide walk's pilot measured slower, rt_api.hip setup_pilot):
+    // the 4-wide instantiations are one-pass and carry none of the pass code
+    const int pass = WIDE ? 0 : F.pass;
     Cnt c{};
     const LaunchConst& C = *lconst;
     const float4* nodes = S.nodes;
@@ -419,7 +422,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WIDE ?
     int phase = FETCH;
     bool tracing = false;
     PixelQueue pq;
-    pq.per = (F.handout && F.pass != 2) ? (unsigned)((F.nloc + kGroups - 1) / kGroups) : 0u;   // pass 2: cost order, interleaved
+    pq.per = (F.handout && pass != 2) ? (unsigned)((F.nloc + kGroups - 1) / kGroups) : 0u;   // pass 2: cost order, interleaved
     FastRay T;
     T.item = 0; T.soff = 0; T.bk = 1000.0f; T.bt = -1; T.brank = -1; T.any = false;
     T.o = rtm_v3(0, 0, 0); T.d = rtm_v3(0, 0, 1); T.ix = T.iy = T.iz = 0.0f;
@@ -443,8 +446,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WIDE ?
     // slice before it (phase WAIT_SLICE), the job's slice index
     // (one-pass launches, and pass 2 of a pilot launch: the samples after the pilot's sb = F.pilot; slice k
     // of a pixel ends at sb + (k + 1) (spp - sb) / nsl)
-    const unsigned nsl = (TS == 1 && F.slices > 1 && F.pass != 1) ? (unsigned)F.slices : 1u;
-    const int sb = F.pass == 2 ? F.pilot : 0;
+    const unsigned nsl = (TS == 1 && F.slices > 1 && pass != 1) ? (unsigned)F.slices : 1u;
+    const int sb = pass == 2 ? F.pilot : 0;
     auto slice_end = [&](unsigned k) { return sb + (int)((k + 1u) * (unsigned)(spp - sb) / nsl); };
     int lim = spp;
     // The deterministic prefix of the pixel's samples (FrameParams::fixed_point; BVH2 walk): a sample's
@@ -501,7 +504,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WIDE ?
         if (COUNT) c.samples++;
         ++s;
         if (s >= spp) write_pixel();
-        const bool stop = (F.pass == 1 && (s >= spp || s >= F.pilot)) || (nsl > 1 && s >= lim);
+        const bool stop = (pass == 1 && (s >= spp || s >= F.pilot)) || (nsl > 1 && s >= lim);
         if (stop) {
             if (nsl > 1) save_slice();
             else save_pilot();
@@ -551,7 +554,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WIDE ?
                 const unsigned q = sl < nsl ? qj - sl * nloc : nloc;
                 bool ok = q < nloc;
                 if (ok) {
-                    p = F.pass == 2 ? (int)F.pilot_order[q] : (int)q;
+                    p = pass == 2 ? (int)F.pilot_order[q] : (int)q;
                     const int krow = p / W;
                     const int col = p - krow * W;
                     const int64_t i64 = ((int64_t)F.row0 + (int64_t)krow * F.row_step) * W + col;
@@ -573,7 +576,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WIDE ?
                     if (sl > 0) {
                         lim = (int)sl;   // continues the pixel once slice sl - 1 is done (below)
                         phase = WAIT_SLICE;
-                    } else if (F.pass == 2) {   // continue from the pilot state: camera hit cached, sample s next
+                    } else if (pass == 2) {   // continue from the pilot state: camera hit cached, sample s next
                         const float4 a = F.pilot_state[2 * (int64_t)p], b = F.pilot_state[2 * (int64_t)p + 1];
                         acc = rtm_v3(a.x, a.y, a.z);
                         kc = a.w;
@@ -593,7 +596,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WIDE ?
                     }
                 } else {
                     // past the tile, or (pass 2, pixels in cost order) a padding pixel past the frame
-                    phase = (F.pass == 2 && q < nloc) ? FETCH : DONE;
+                    phase = (pass == 2 && q < nloc) ? FETCH : DONE;
                 }
             }
         }
