@@ -134,9 +134,17 @@ __device__ Hit trace_ref(const DevScene& S, rtm_f3 o, rtm_f3 d, int* __restrict_
 // scaled by 1/d instead of divided by d (MathLib.cl:167-199).
 __device__ __forceinline__ void slab(float lo_x, float hi_x, float lo_y, float hi_y, float lo_z, float hi_z,
                                      rtm_f3 o, float ix, float iy, float iz, float& tmin, float& tmax) {
+#ifdef RT_FMA_SLAB
+    // variant (A/B): fma(b, 1/d, -o/d), the ray's -o/d shared by every box of a step (one fma per bound)
+    const float nx = -o.x * ix, ny = -o.y * iy, nz = -o.z * iz;
+    const float x0 = fmaf(lo_x, ix, nx), x1 = fmaf(hi_x, ix, nx);
+    const float y0 = fmaf(lo_y, iy, ny), y1 = fmaf(hi_y, iy, ny);
+    const float z0 = fmaf(lo_z, iz, nz), z1 = fmaf(hi_z, iz, nz);
+#else
     const float x0 = (lo_x - o.x) * ix, x1 = (hi_x - o.x) * ix;
     const float y0 = (lo_y - o.y) * iy, y1 = (hi_y - o.y) * iy;
     const float z0 = (lo_z - o.z) * iz, z1 = (hi_z - o.z) * iz;
+#endif
     tmin = fmaxf(fmaxf(fminf(x0, x1), fminf(y0, y1)), fminf(z0, z1));
     tmax = fminf(fminf(fmaxf(x0, x1), fmaxf(y0, y1)), fmaxf(z0, z1));
 }
