@@ -134,17 +134,9 @@ __device__ Hit trace_ref(const DevScene& S, rtm_f3 o, rtm_f3 d, int* __restrict_
 // scaled by 1/d instead of divided by d (MathLib.cl:167-199).
 __device__ __forceinline__ void slab(float lo_x, float hi_x, float lo_y, float hi_y, float lo_z, float hi_z,
                                      rtm_f3 o, float ix, float iy, float iz, float& tmin, float& tmax) {
-#ifdef RT_FMA_SLAB
-    // variant (A/B): fma(b, 1/d, -o/d), the ray's -o/d shared by every box of a step (one fma per bound)
-    const float nx = -o.x * ix, ny = -o.y * iy, nz = -o.z * iz;
-    const float x0 = fmaf(lo_x, ix, nx), x1 = fmaf(hi_x, ix, nx);
-    const float y0 = fmaf(lo_y, iy, ny), y1 = fmaf(hi_y, iy, ny);
-    const float z0 = fmaf(lo_z, iz, nz), z1 = fmaf(hi_z, iz, nz);
-#else
     const float x0 = (lo_x - o.x) * ix, x1 = (hi_x - o.x) * ix;
     const float y0 = (lo_y - o.y) * iy, y1 = (hi_y - o.y) * iy;
     const float z0 = (lo_z - o.z) * iz, z1 = (hi_z - o.z) * iz;
-#endif
     tmin = fmaxf(fmaxf(fminf(x0, x1), fminf(y0, y1)), fminf(z0, z1));
     tmax = fminf(fminf(fmaxf(x0, x1), fmaxf(y0, y1)), fmaxf(z0, z1));
 }
@@ -480,11 +472,6 @@ __device__ Hit trace_brute_compact(const DevScene& S, rtm_f3 o, rtm_f3 d, char* 
         // to back, then the passes are queued (culling uses the best hit as of the group's start:
         // conservative)
         const ConstF4 cb = as_const(S.brute_box);
-#ifdef RT_BRUTE_FMA
-        // variant: (b - o) / d as fma(b, 1/d, -o/d), one rounding of the loop-invariant -o/d per ray (A/B only:
-        // a different rounding at box faces than the tree walk's slab)
-        const float nox = -o.x * ix, noy = -o.y * iy, noz = -o.z * iz;
-#endif
         for (int g0 = 0; g0 < S.nbox; g0 += kBoxGroup) {
             float4 bx[2 * kBoxGroup];
 #pragma unroll
@@ -494,16 +481,8 @@ __device__ Hit trace_brute_compact(const DevScene& S, rtm_f3 o, rtm_f3 d, char* 
 #pragma unroll
             for (int j = 0; j < kBoxGroup; ++j) {
                 float tn, tx;
-#ifdef RT_BRUTE_FMA
-                const float x0 = fmaf(bx[2 * j].x, ix, nox), x1 = fmaf(bx[2 * j].y, ix, nox);
-                const float y0 = fmaf(bx[2 * j].z, iy, noy), y1 = fmaf(bx[2 * j].w, iy, noy);
-                const float z0 = fmaf(bx[2 * j + 1].x, iz, noz), z1 = fmaf(bx[2 * j + 1].y, iz, noz);
-                tn = fmaxf(fmaxf(fminf(x0, x1), fminf(y0, y1)), fminf(z0, z1));
-                tx = fminf(fminf(fmaxf(x0, x1), fmaxf(y0, y1)), fmaxf(z0, z1));
-#else
                 slab(bx[2 * j].x, bx[2 * j].y, bx[2 * j].z, bx[2 * j].w, bx[2 * j + 1].x, bx[2 * j + 1].y, o, ix, iy,
                      iz, tn, tx);
-#endif
                 pass[j] = box_hit(tn, tx, cull);
             }
 #pragma unroll
