@@ -1073,6 +1073,7 @@ namespace {
 // (teams + trails); C4 N=1 303.6 / 284.8, N=2 181.5 / 254.9 (3/4 of C4's pixels are sky, finished by
 // the pilot pass: the rest is one pixel per lane, where trails win), N=4 121.4 / 318.4
 constexpr int kSlicesWide = 8;
+constexpr int kSlicesWideSmall = 12;
 constexpr int64_t kSlicesMinPerLane = 4;
 
 // Two-pass launches (FrameParams::pass): FAST tree-walk renders of tiles with more pixels than the
@@ -1168,6 +1169,11 @@ hipError_t setup_slices(rt_ctx* ctx, Device& d, rt::FrameParams& fp, hipStream_t
     // (pilot_team_pick_kernel: more unfinished pixels than lanes); the team and trail kernels take none
     int k = ctx->slices > 0 ? ctx->slices
                             : (use_wide(ctx) || fp.pilot > 0 || fp.nloc >= kSlicesMinPerLane * lanes) ? kSlicesWide : 1;
+    // the 4-wide walk's small tiles (under kSlicesMinPerLane pixels per resident lane: C5's eighth, 2.26) take
+    // finer slices: 1/8 tile 629.7 / 620.8 ms at 8 / 12 (whole frame 4,594 / 4,612: 8 kept there)
+    if (ctx->slices < 0 && use_wide(ctx) &&
+        fp.nloc < kSlicesMinPerLane * (int64_t)std::max(d.cus, 1) * rt::kWideWaves * 4 * 64)
+        k = kSlicesWideSmall;
     k = std::min(k, (fp.spp - std::max(fp.pilot, 0)) / 2);   // every slice at least two samples
     if (k <= 1 || (int64_t)fp.nloc * k >= ((int64_t)1 << 32)) return hipSuccess;
     const size_t n = (size_t)fp.nloc;

@@ -12,6 +12,10 @@ constexpr int kStackLds = 20;
 // 11 entries (88 B per lane) leave the LDS room for them (C5 at 7 waves: 5,890 ms with 11 entries,
 // 5,915 with 10)
 constexpr int kStackLdsWide = 11;
+#ifndef RT_WIDE_WAVES
+#define RT_WIDE_WAVES 7   // variant builds (tools/variants.py) override it for the spill A/B
+#endif
+constexpr int kWideWaves = RT_WIDE_WAVES;   // waves per SIMD of the 4-wide walk (rt_kernels.hip)
 constexpr int kNodeF4 = 4;             // float4 per FAST BVH2 node (DevScene::nodes)
 constexpr int kMaxLanesPerCu = 2048;   // resident threads per CU (gfx950)
 #ifndef RT_BOX_GROUP

@@ -365,10 +365,7 @@ constexpr size_t kStepMaxBytes = 16u << 20;
 // them.  C5 ms per frame at 4 / 5 / 6 / 7 / 8 waves: 7,214 / 6,432 / 6,045 / 5,890 / 6,040.  The
 // BVH2 walk (C3/C4) is bound by the vector memory pipeline and keeps 4 waves with its whole 20-entry
 // stack in LDS (5 waves with a 14-entry spilling stack: C3 149 -> 157 ms, C4 475 -> 502 ms).
-#ifndef RT_WIDE_WAVES
-#define RT_WIDE_WAVES 7   // variant builds (tools/variants.py) override it for the spill A/B
-#endif
-constexpr int kWideWaves = RT_WIDE_WAVES;
+// (kWideWaves: rt_internal.h)
 
 // TS > 1: teams of TS lanes per pixel walk each ray together (team_step; BVH2 item steps only).
 // F.walk_team_dev (pass 2 of a pilot launch): the team size was chosen on the device from the pixels
