@@ -83,15 +83,20 @@ def main(prof, tag, workload, frames=None, kernel=KERNEL, wave_stats=None):
             s["kernel_calls"] = calls
             s["frames"] = int(frames) if frames else calls
             s["kernel_avg_ms"] = total / 1e6 / s["frames"]
-    counters = {}
+    counters, dispatches = {}, {}
     for sub in GROUPS:
         for r in _rows(os.path.join(where[sub], "*counter_collection.csv")):
             if re.search(kernel, r["Kernel_Name"]):
                 counters.setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))
-    nframes = max(1, s.get("frames", 1))
+                dispatches.setdefault(r["Counter_Name"], set()).add(r["Dispatch_Id"])
+    # dispatches per frame from the kernel trace; a pass may render a different number of frames than
+    # the kernel-trace run (e.g. 20 timed steps traced, 1 per counter pass), so each counter is divided
+    # by the frames of its own pass
+    per_frame = s.get("kernel_calls", 1) / max(1, s.get("frames", 1))
     for k, v in sorted(counters.items()):
-        # per frame: every dispatch of the frame summed (the profiled run renders `frames` frames)
-        s[k + "_per_launch"] = float(np.sum(v)) / nframes
+        # per frame: every dispatch of the frame summed
+        nfr = max(1.0, len(dispatches[k]) / per_frame)
+        s[k + "_per_launch"] = float(np.sum(v)) / nfr
         s[k + "_launches"] = len(v)
     g = lambda k: s.get(k + "_per_launch")  # noqa: E731
     if g("TCC_EA0_RDREQ_128B_sum") is not None:
