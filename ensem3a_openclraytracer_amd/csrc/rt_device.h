@@ -902,7 +902,7 @@ struct FastRay {
     int item;
     unsigned soff;    // stack top, bytes
     float bk;         // best distance
-    int bt;           // best triangle's byte offset (48 t), -1 = none
+    int bt;           // best triangle's reference index (BVH2 walks; 48 x it on the 4-wide walk), -1 = none
     int brank;        // its rank in the reference DFS order
     bool any;         // any hit ends the ray (a shadow ray whose hit only matters as hit / miss)
 };
@@ -950,7 +950,7 @@ __device__ __forceinline__ bool fast_round(const DevScene& S, FastRay& R, const 
         if (mt_flat(tb, toff, R.o, R.d, &k, &rank, &index) && k > 0.0001f &&
             (k < R.bk || (k == R.bk && rank < R.brank))) {
             R.bk = k;
-            R.bt = 48 * index;
+            R.bt = index;
             R.brank = rank;
             if (R.any) return true;
         }
@@ -1006,13 +1006,15 @@ __device__ __forceinline__ bool fast_step(const DevScene& S, FastRay& R, const c
     float k;
     int rank;
     const bool mt = mt_vals(g0, g1, leaf_e2(g2, e), R.o, R.d, &k, &rank);
-    const bool take = !node && mt && k > 0.0001f && (k < R.bk || (k == R.bk && rank < R.brank));
+    // bitwise, not short-circuit: the compiler keeps && / || here as nested exec-mask branches (~14 SALU
+    // per step on the wave's own issue slots)
+    const bool take = (!node) & mt & (k > 0.0001f) & ((k < R.bk) | ((k == R.bk) & (rank < R.brank)));
     if (COUNT) {
         if (node) { c.nodes++; c.boxes += 2; }
         else c.tris++;
     }
     R.bk = take ? k : R.bk;
-    R.bt = take ? 48 * __float_as_int(g1.w) : R.bt;   // e1.w: the triangle's reference index
+    R.bt = take ? __float_as_int(g1.w) : R.bt;   // e1.w: the triangle's reference index
     R.brank = take ? rank : R.brank;
     const bool first0 = t0n <= t1n;
     if (h0 && h1) {   // the farther child waits on the stack
@@ -1122,13 +1124,13 @@ __device__ __forceinline__ bool team_step(int ts, FastRay& R, unsigned& boff, co
         float k;
         int rank;
         const bool mt = mt_vals(g0, g1, leaf_e2(g2, e), R.o, R.d, &k, &rank);
-        improved = !node && mt && k > 0.0001f && (k < R.bk || (k == R.bk && rank < R.brank));
+        improved = (!node) & mt & (k > 0.0001f) & ((k < R.bk) | ((k == R.bk) & (rank < R.brank)));
         if (COUNT) {
             if (node) { c.nodes++; c.boxes += 2; }
             else c.tris++;
         }
         R.bk = improved ? k : R.bk;
-        R.bt = improved ? 48 * __float_as_int(g1.w) : R.bt;
+        R.bt = improved ? __float_as_int(g1.w) : R.bt;
         R.brank = improved ? rank : R.brank;
         const bool first0 = t0n <= t1n;
         if (h0 && h1) {
@@ -1235,7 +1237,9 @@ __device__ __forceinline__ bool wide_leaf(float4 g0, float4 g1, float4 g2, float
         mt_core(rtm_v3(g1.z, g1.w, g2.x), rtm_v3(g2.y, g2.z, g2.w), rtm_v3(g3.x, g3.y, g3.z), R.o, R.d, &k);
     const bool take = on & bh & mt & (k > 0.0001f) & ((k < R.bk) | ((k == R.bk) & (rank < R.brank)));
     R.bk = take ? k : R.bk;
-    R.bt = take ? 48 * __float_as_int(g3.w) : R.bt;   // the triangle's reference index
+    // the 4-wide walk keeps 48 x the index (its consumer divides): the plain index changed the register
+    // allocation of its 72-VGPR kernel for the worse (51 instead of 36 spilled, one scratch access in the loop)
+    R.bt = take ? 48 * __float_as_int(g3.w) : R.bt;
     R.brank = take ? rank : R.brank;
     return take && R.any;
 }

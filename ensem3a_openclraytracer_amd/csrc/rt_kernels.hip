@@ -629,7 +629,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WIDE ?
 
         // -- advance every lane without a ray in flight until it needs one --
         if (!tracing && phase != DONE && phase != FETCH) {
-            Hit h{T.bk, T.bt >= 0 ? (int)((unsigned)T.bt / 48u) : -1};
+            Hit h{T.bk, WIDE && T.bt >= 0 ? (int)((unsigned)T.bt / 48u) : T.bt};
             if (phase == PRIMARY) {
                 tc = h.tri;
                 kc = h.k;

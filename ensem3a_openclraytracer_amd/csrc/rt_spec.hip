@@ -330,7 +330,7 @@ spec_kernel(DevScene S, FrameParams F, float* __restrict__ out, unsigned int* __
                 restart_sample();
             };
             // the traced ray's result (render_resume_kernel: BOUNCE / SUN)
-            Hit h{T.bk, T.bt >= 0 ? (int)((unsigned)T.bt / 48u) : -1};
+            Hit h{T.bk, T.bt};
             if (phase == BOUNCE) {
                 if (h.tri >= 0) {
                     tri = h.tri;
