@@ -1038,6 +1038,68 @@ __device__ __forceinline__ bool fast_step(const DevScene& S, FastRay& R, const c
     return true;
 }
 
+// ---- software-pipelined item step (render_resume_kernel's BVH2 walk with one lane per ray) ----
+// fast_step with the next item's four loads issued before this item's leaf test: the node test and
+// the pop (culled against the best hit as it was before this step's leaf test -- a conservative cull:
+// an entry the new best would cull is fetched and its children culled one step later) decide the next
+// item, its loads go out, and the Moller-Trumbore arithmetic of the current item runs while they are
+// in flight.  The accepted triangles are fast_step's (the acceptance test is unchanged), so the hit is.
+struct ItemData {
+    float4 g0, g1, g2;
+    int2 e;
+};
+template <bool SOA>
+__device__ __forceinline__ ItemData item_fetch(int item, const char* nb, const char* tb, unsigned kstride) {
+    const bool node = item >= 0;
+    const char* p = node ? nb + (SOA ? 16u : 16u * kNodeF4) * (unsigned)item : tb + ~(unsigned)item;
+    const unsigned ks = node ? kstride : 16u;
+    ItemData D;
+    D.g0 = *reinterpret_cast<const float4*>(p);
+    D.g1 = *reinterpret_cast<const float4*>(p + ks);
+    D.g2 = *reinterpret_cast<const float4*>(p + 2 * ks);
+    D.e = *reinterpret_cast<const int2*>(p + (node ? 3 * ks : kLeafTail));
+    return D;
+}
+template <bool COUNT, bool SOA, bool OVF>
+__device__ __forceinline__ bool fast_step_pipe(FastRay& R, ItemData& D, const char* nb, const char* tb,
+                                               const LaneStack& st, unsigned kstride, Cnt& c) {
+    const bool node = R.item >= 0;
+    const float4 g0 = D.g0, g1 = D.g1, g2 = D.g2;
+    const int2 e = D.e;
+    if (COUNT) count_wave(c.wave_trav);
+    const float cull = R.bk * CULL_MARGIN;
+    float t0n, t0x, t1n, t1x;
+    slab(g0.x, g0.y, g0.z, g0.w, g2.x, g2.y, R.o, R.ix, R.iy, R.iz, t0n, t0x);
+    slab(g1.x, g1.y, g1.z, g1.w, g2.z, g2.w, R.o, R.ix, R.iy, R.iz, t1n, t1x);
+    const bool h0 = node && box_hit(t0n, t0x, cull), h1 = node && box_hit(t1n, t1x, cull);
+    const bool first0 = t0n <= t1n;
+    if (h0 && h1) {
+        st.template put<OVF>(R.soff, make_int2(first0 ? e.y : e.x, __float_as_int(first0 ? t1n : t0n)));
+        R.soff += st.stride;
+    }
+    int next = (h0 && h1) ? (first0 ? e.x : e.y) : h0 ? e.x : h1 ? e.y : INT_MIN;
+    while (next == INT_MIN && R.soff > 0) {
+        R.soff -= st.stride;
+        const int2 en = st.template get<OVF>(R.soff);
+        if (__int_as_float(en.y) <= cull) next = en.x;
+    }
+    const bool done = next == INT_MIN;
+    if (!done) D = item_fetch<SOA>(next, nb, tb, kstride);
+    float k;
+    int rank;
+    const bool mt = mt_vals(g0, g1, leaf_e2(g2, e), R.o, R.d, &k, &rank);
+    const bool take = (!node) & mt & (k > 0.0001f) & ((k < R.bk) | ((k == R.bk) & (rank < R.brank)));
+    if (COUNT) {
+        if (node) { c.nodes++; c.boxes += 2; }
+        else c.tris++;
+    }
+    R.bk = take ? k : R.bk;
+    R.bt = take ? __float_as_int(g1.w) : R.bt;
+    R.brank = take ? rank : R.brank;
+    R.item = done ? R.item : next;
+    return done | (take & R.any);
+}
+
 // ---- team traversal: TS lanes walk one ray (tiles with about one pixel per lane, option "walk_team") ----
 // When a tile has no more pixels than the device has lanes, a frame lasts as long as its slowest
 // pixel's chain of samples, and a chain advances one dependent node fetch per step.

@@ -763,8 +763,15 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WIDE ?
         // of the lanes still rendering (all 64 until the pixel counters run dry)
         const unsigned long long alive = __ballot(phase != DONE);
         const int rthr = F.resume_min * __popcll(alive);
+        // BVH2 item steps of single lanes are software-pipelined (fast_step_pipe: the next item's loads go
+        // out before this item's leaf test; r05: C3 114.4 -> 110.5 ms, C4 282.7 -> 284.6 ms); the loads
+        // for the first step of this round are issued here (a lane continuing its ray re-fetches its item)
+        constexpr bool PIPE = STEP && !WIDE && TS == 1;
+        ItemData D;
+        if (PIPE && tracing) D = item_fetch<SMEM>(T.item, nb, tb, kstride);
         while (true) {
-            if (tracing && (TS > 1 ? team_step<COUNT, SMEM, OVF>(TS, T, boff, nb, tb, lst, kstride, c)
+            if (tracing && (PIPE ? fast_step_pipe<COUNT, SMEM, OVF>(T, D, nb, tb, lst, kstride, c)
+                            : TS > 1 ? team_step<COUNT, SMEM, OVF>(TS, T, boff, nb, tb, lst, kstride, c)
                             : WIDE ? (STEP ? wide_step<COUNT, OVF>(T, wnb, wlb, lst, c)
                                            : wide_round<COUNT, OVF>(T, wnb, wlb, lst, c))
                             : STEP ? fast_step<COUNT, SMEM, OVF>(S, T, nb, tb, lst, kstride, c)
