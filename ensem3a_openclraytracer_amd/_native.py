@@ -300,7 +300,7 @@ class Context:
         out = np.zeros(8, dtype=np.int64)
         self._check(lib().rt_debug_scene_info(self.handle, out.ctypes.data))
         return dict(fast_ok=bool(out[0]), depth=int(out[1]), nodes=int(out[2]), tris=int(out[3]),
-                    brute_records=int(out[4]), brute_boxes=int(out[5]))
+                    brute_records=int(out[4]), brute_boxes=int(out[5]), wdq_omax=int(out[6]) * 1e-6)
 
 
 def parse_obj(text):

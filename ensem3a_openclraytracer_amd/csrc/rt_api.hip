@@ -69,6 +69,7 @@ struct HostScene {
     std::vector<float> wnodes;     // wide layout: 16 floats per 4-wide node (DevScene::wnodes)
     std::vector<float> wleaves;    // wide layout: 16 floats per leaf, in reference DFS rank order
     int32_t nwnodes = 0, wroot_ref = 0, wdepth = 1;
+    float wdq_omax = 0.0f;   // the 4-wide layout's dequantisation gap covers ray origins up to this (0: no gap)
     std::vector<float> bvh9;
     std::vector<float> tri_geo;    // 12 floats per triangle
     std::vector<float> tri_fast;   // tri_geo's records in FAST leaf order (DevScene::tri_fast)
@@ -113,6 +114,7 @@ struct rt_ctx {
     int stack_lds = 0;    // FAST stack entries per lane kept in LDS (0 = auto: rt::kStackLds, kStackLdsWide)
     int ref_stack = 20;   // REF traversal stack capacity (20 = the reference's, stack.cl:4)
     int spec = -1;        // small tiles: speculative trails per pixel in pass 2 (0 = off, 2, 4 or 8, -1 = auto)
+    int wdq = 1;          // 4-wide walk: origin-folded dequantisation where the builder's gap covers the frame (option "wdq")
     int handout = -1;     // pixel hand-out: 0 = interleaved chunks, 1 = a contiguous block per XCD group, -1 = auto
     int slices = -1;      // one-pass tree-walk launches: sample slices per pixel (FrameParams::slices; 0 off, -1 auto)
     std::string err;
@@ -190,26 +192,36 @@ inline float deq(float p, uint32_t q, float s) { return p + (float)q * s; }
 // biased exponent byte (scale = as_float(e << 23)), or -1 when no exponent up to 2^100 gives
 // containing bounds (non-finite bounds, or an extent beyond 255 * 2^100): the caller must then not
 // use the quantised layout (a dequantised box that is not a superset could cull a hit subtree).
-extern "C" int rt_debug_quantise_axis(float p, const float* lo, const float* hi, int n, uint8_t* qlo, uint8_t* qhi) {
+extern "C" int rt_debug_quantise_axis(float p, const float* lo, const float* hi, int n, float gap, uint8_t* qlo,
+                                      uint8_t* qhi) {
     if (n < 1 || n > 4 || !lo || !hi || !qlo || !qhi) return -1;
-    if (!std::isfinite(p)) return -1;
+    if (!std::isfinite(p) || !std::isfinite(gap) || gap < 0.0f) return -1;
     double ext = 0.0;
     for (int c = 0; c < n; ++c) {
         if (!std::isfinite(lo[c]) || !std::isfinite(hi[c])) return -1;
-        ext = std::max(ext, (double)hi[c] - (double)p);
+        ext = std::max(ext, (double)hi[c] + gap - (double)p);
     }
     int e = ext > 0.0 ? (int)std::ceil(std::log2(ext / 255.0)) : -100;
     e = std::min(std::max(e, -100), 100);
+    // a bound with q > 0 lies at least `gap` outside its child's exact bound, in exact arithmetic (the
+    // kernels' origin-folded form fma(q, s, p - o) is then conservative, rt_device.h wide_node); q = 0
+    // is the corner p itself, which both forms dequantise exactly
+    auto lo_ok = [&](uint32_t q, float sc, float l) {
+        return deq(p, q, sc) <= l && (q == 0 || (double)p + (double)q * sc <= (double)l - gap);
+    };
+    auto hi_ok = [&](uint32_t q, float sc, float h) {
+        return deq(p, q, sc) >= h && (q == 0 ? (double)p >= h : (double)p + (double)q * sc >= (double)h + gap);
+    };
     for (;; ++e) {
         const float sc = std::ldexp(1.0f, e);
         bool ok = true;
         for (int c = 0; c < n && ok; ++c) {
-            double fl = std::floor(((double)lo[c] - p) / sc), fh = std::ceil(((double)hi[c] - p) / sc);
+            double fl = std::floor(((double)lo[c] - gap - p) / sc), fh = std::ceil(((double)hi[c] + gap - p) / sc);
             uint32_t a = (uint32_t)std::min(255.0, std::max(0.0, fl));
             uint32_t b = (uint32_t)std::min(255.0, std::max(0.0, fh));
-            while (a > 0 && deq(p, a, sc) > lo[c]) --a;
-            while (b < 255 && deq(p, b, sc) < hi[c]) ++b;
-            ok = deq(p, a, sc) <= lo[c] && deq(p, b, sc) >= hi[c];
+            while (a > 0 && !lo_ok(a, sc, lo[c])) --a;
+            while (b < 255 && !hi_ok(b, sc, hi[c])) ++b;
+            ok = lo_ok(a, sc, lo[c]) && hi_ok(b, sc, hi[c]);
             qlo[c] = (uint8_t)a;
             qhi[c] = (uint8_t)b;
         }
@@ -237,6 +249,7 @@ void emit_wide(HostScene& hs, const int32_t* L, const int32_t* R, const int32_t*
     hs.nwnodes = 0;
     hs.wroot_ref = 0;
     hs.wdepth = 1;
+    hs.wdq_omax = 0.0f;
     if (hs.ntri > (1 << 25)) return;   // leaf refs ~(64 * rank) must fit 31 bits: no wide layout
     auto is_inner = [&](int64_t i) { return L[i] >= 0; };
     auto area = [&](int64_t i) {
@@ -286,6 +299,17 @@ void emit_wide(HostScene& hs, const int32_t* L, const int32_t* R, const int32_t*
         if (!is_inner(i) && T[i] >= 0) nleaves = std::max(nleaves, rank_of((int32_t)i) + 1);
     hs.wleaves.assign((size_t)std::max(nleaves, 1) * 16, 0.0f);
     auto leaf_ref = [&](int32_t c) { return ~(64 * rank_of(c)); };
+    // the gap of the origin-folded dequantisation: every child bound with q > 0 is
+    // quantised at least gap = 2^-17 P outside the exact bound, P = the largest coordinate magnitude of
+    // the leaf boxes; that covers the rounding of fma(q, s, p - o) for ray origins up to ~20 P (hit
+    // points, and cameras up to DevScene::wdq_omax, checked per frame).  If a node cannot take the gap
+    // (no exponent up to 2^100), the whole layout is quantised without it and the exact form runs.
+    double pmax = 0.0, bmax = 0.0;   // bmax: the largest |p + q s| the layout holds
+    for (int64_t i = 0; i < nn; ++i)
+        for (int k = 0; k < 6; ++k) pmax = std::max(pmax, (double)std::fabs(box[6 * i + k]));
+    float gap = (std::isfinite(pmax) && pmax > 0x1p-100) ? (float)std::ldexp(pmax, -17) : 0.0f;
+retry:
+    bmax = 0.0;
     for (size_t w = 0; w < bfs.size(); ++w) {
         float* o = hs.wnodes.data() + 16 * w;
         const auto& ch = children[w];
@@ -303,7 +327,11 @@ void emit_wide(HostScene& hs, const int32_t* L, const int32_t* R, const int32_t*
         uint8_t ql[3][4] = {}, qh[3][4] = {};
         uint32_t meta = 0;
         for (int a = 0; a < 3; ++a) {
-            const int ex = rt_debug_quantise_axis(p[a], lo[a], hi[a], n, ql[a], qh[a]);
+            const int ex = rt_debug_quantise_axis(p[a], lo[a], hi[a], n, gap, ql[a], qh[a]);
+            if (ex < 0 && gap > 0.0f) {   // no room for the gap: quantise without it, exact form only
+                gap = 0.0f;
+                goto retry;
+            }
             if (ex < 0) {   // no containing quantisation: no wide layout (use_wide() keeps the BVH2 walk)
                 hs.wnodes.clear();
                 hs.wleaves.clear();
@@ -313,6 +341,9 @@ void emit_wide(HostScene& hs, const int32_t* L, const int32_t* R, const int32_t*
                 return;
             }
             meta |= (uint32_t)ex << (8 * a);
+            const double sc = std::ldexp(1.0, ex - 127);
+            for (int c = 0; c < n; ++c)
+                bmax = std::max(bmax, std::max(std::fabs(p[a] + ql[a][c] * sc), std::fabs(p[a] + qh[a][c] * sc)));
         }
         o[0] = p[0]; o[1] = p[1]; o[2] = p[2]; o[3] = as_f32((int32_t)meta);
         for (int c = 0; c < 4; ++c)
@@ -324,6 +355,14 @@ void emit_wide(HostScene& hs, const int32_t* L, const int32_t* R, const int32_t*
         };
         o[8] = pack(ql[0]); o[9] = pack(ql[1]); o[10] = pack(ql[2]); o[11] = pack(qh[0]);
         o[12] = pack(qh[1]); o[13] = pack(qh[2]); o[14] = 0.0f; o[15] = 0.0f;
+    }
+    // origins the gap covers: gap >= u (1 + u) (|p - o| + |p + q s - o| + |b - o|) for every bound, u = 2^-24,
+    // with |p|, |b| <= pmax and |p + q s| <= bmax holds for |o| <= (gap / (u (1 + u)) - 2 pmax - bmax) / 3
+    // (about 40 pmax); kept 1/2 below that
+    {
+        const double u = 0x1p-24;
+        const double om = gap > 0.0f ? ((double)gap / (u * (1.0 + u)) - 2.0 * pmax - bmax) / 3.0 : 0.0;
+        hs.wdq_omax = om > 0.0 ? (float)(0.5 * om) : 0.0f;
     }
     for (int64_t i = 0; i < nn; ++i) {
         if (is_inner(i) || T[i] < 0) continue;
@@ -572,6 +611,23 @@ bool pack_fast(HostScene& hs, const float* bvh9, int64_t nn, int64_t ntri, int l
 void pack_checked(HostScene& hs, const float* bvh9, int64_t nb, int64_t ntri, int layout, int brute_max,
                   std::string& why) {
     hs.fast_ok = (ntri > 0) ? pack_fast(hs, bvh9, nb, ntri, layout, brute_max, why) : true;
+    if (hs.fast_ok && ntri > 0) {
+        // the FAST kernels' Moller-Trumbore reciprocal (rt_device.h mt_recip) is IEEE-exact for
+        // |a| <= 2^126, a = e1 . (d x e2) with |d| = 1: bound |e1| |e2| (finite edges; an infinite or
+        // NaN edge makes a infinite or NaN, which mt_recip also returns exactly) 64x below it
+        double m1 = 0.0, m2 = 0.0;
+        for (int64_t t = 0; t < ntri; ++t) {
+            const float* g = hs.tri_geo.data() + 12 * t;
+            const double l1 = std::sqrt((double)g[4] * g[4] + (double)g[5] * g[5] + (double)g[6] * g[6]);
+            const double l2 = std::sqrt((double)g[8] * g[8] + (double)g[9] * g[9] + (double)g[10] * g[10]);
+            if (std::isfinite(l1)) m1 = std::max(m1, l1);
+            if (std::isfinite(l2)) m2 = std::max(m2, l2);
+        }
+        if (!(m1 * m2 <= std::ldexp(1.0, 120))) {
+            hs.fast_ok = false;
+            why = "triangle edges beyond 2^60 (the FAST reciprocal needs |e1 . (d x e2)| <= 2^126)";
+        }
+    }
     if (ntri == 0) {
         hs.nnodes = 0; hs.root_ref = 0; hs.depth = 1; hs.nodes.clear();
         hs.nwnodes = 0; hs.wroot_ref = 0; hs.wdepth = 1; hs.wnodes.clear(); hs.wleaves.clear();
@@ -638,6 +694,7 @@ rt::DevScene dev_scene(const rt_ctx* ctx, const Device& d) {
     s.wnodes = wide ? (const float4*)d.wnodes.p : nullptr;
     s.wleaves = wide ? (const float4*)d.wleaves.p : nullptr;
     s.wroot_ref = ctx->hs.wroot_ref;
+    s.wdq_omax = wide ? ctx->hs.wdq_omax : 0.0f;
     for (int k = 0; k < 6; ++k) s.root_box[k] = ctx->hs.root_box[k];
     s.bvh9 = (const float*)d.bvh9.p;
     s.nbvh9 = ctx->hs.nbvh9;
@@ -690,6 +747,7 @@ int check_frame(rt_ctx* ctx, const float* cam, const float* env, int64_t npix, i
     fp->sun_skip = (ctx->sun_skip && env[3] == 0.0f && env[4] >= 0.0f && ctx->hs.colors_finite) ? 1 : 0;
     fp->sun_any = (ctx->sun_any && !ctx->hs.has_glass) ? 1 : 0;
     fp->wide = use_wide(ctx) ? 1 : 0;
+    fp->wdq = ctx->wdq;
     fp->fixed_point = ctx->fixed_point;
     fp->sun_cache = ctx->fixed_point && ctx->sun_cache ? 1 : 0;
     fp->pass = 0;
@@ -902,6 +960,11 @@ int rt_set_option(rt_ctx* ctx, const char* key, int64_t value) {
     if (!std::strcmp(key, "slices")) {
         if (value < -1 || value > 16) return set_err(ctx, RT_ERR_ARG, "slices must be -1 (auto), 0 (off) or 1..16");
         ctx->slices = (int)value;
+        return RT_OK;
+    }
+    if (!std::strcmp(key, "wdq")) {
+        if (value != 0 && value != 1) return set_err(ctx, RT_ERR_ARG, "wdq must be 0 or 1");
+        ctx->wdq = (int)value;
         return RT_OK;
     }
     if (!std::strcmp(key, "handout")) {
@@ -1505,7 +1568,8 @@ int rt_debug_scene_info(rt_ctx* ctx, int64_t out[8]) {
     out[3] = ctx->hs.ntri;
     out[4] = effective_traversal(ctx) == RT_TRAVERSAL_FAST ? ctx->hs.nbrute : 0;
     out[5] = out[4] ? ctx->hs.nbox : 0;
-    out[6] = 0;
+    // the 4-wide layout's origin bound of the origin-folded dequantisation, in millionths (0: none)
+    out[6] = ctx->hs.wnodes.empty() ? 0 : (int64_t)std::llround((double)ctx->hs.wdq_omax * 1e6);
     out[7] = 0;
     return RT_OK;
 }

@@ -165,11 +165,23 @@ __device__ __forceinline__ bool mt_flat(const char* __restrict__ tb, unsigned to
 }
 
 // mt_flat on a loaded record (g0 = a.p | rank, g1 = e1, g2 = e2).
+// 1/a of the Moller-Trumbore test in 4 instructions instead of the IEEE division's 11: the v_rcp_f32
+// seed, one Newton step in fma and v_div_fixup (infinities, NaN) give 1.0f / a bit for bit for every
+// a with |a| <= 2^126 -- checked on the MI355X over all 2^32 inputs (tools/rcp_exhaustive.hip,
+// profiles/r05_rcp_exhaustive.json).  Above 2^126 the reciprocal is denormal and the seed flushes it:
+// the FAST path is taken only on scenes whose triangle edges keep |a| = |e1 . (d x e2)| far below
+// 2^126 (rt_api.hip pack_fast; |d| = 1).  |a| < 1e-7 is the parallel case, whose 1/a is not used.
+__device__ __forceinline__ float mt_recip(float a) {
+    const float r = __builtin_amdgcn_rcpf(a);
+    const float e = fmaf(-a, r, 1.0f);
+    return __builtin_amdgcn_div_fixupf(fmaf(e, r, r), a, 1.0f);
+}
+
 // Moller-Trumbore on a triangle given as (a.p, e1, e2): MathLib.cl:117-160's arithmetic.
 __device__ __forceinline__ bool mt_core(rtm_f3 p0, rtm_f3 e1, rtm_f3 e2, rtm_f3 o, rtm_f3 d, float* kout) {
     const rtm_f3 h = rtm_cross(d, e2);
     const float a = rtm_dot(e1, h);
-    const float f = 1.0f / a;
+    const float f = mt_recip(a);
     const rtm_f3 s = rtm_sub(o, p0);
     const float u = f * rtm_dot(s, h);
     const rtm_f3 q = rtm_cross(s, e1);
@@ -432,7 +444,7 @@ __device__ Hit trace_brute_compact(const DevScene& S, rtm_f3 o, rtm_f3 d, char* 
             const rtm_f3 a = rtm_v3(r1.z, r1.w, r2.x), e1 = rtm_v3(r2.y, r2.z, r2.w), e2 = rtm_v3(r3.x, r3.y, r3.z);
             const rtm_f3 h = rtm_cross(rd, e2);
             const float det = rtm_dot(e1, h);
-            const float f = 1.0f / det;
+            const float f = mt_recip(det);
             const rtm_f3 sv = rtm_sub(ro, a);
             const float u = f * rtm_dot(sv, h);
             const rtm_f3 qv = rtm_cross(sv, e1);
@@ -1232,7 +1244,7 @@ __device__ __forceinline__ bool team_step(int ts, FastRay& R, unsigned& boff, co
 // farthest first.  Returns the nearest hit child, or INT_MIN (pop next).
 // PRE0: child 0's entry distance and box test were computed by the caller (tn0, hit0: wide_step's shared
 // slab), the loop tests children 1..3
-template <bool COUNT, bool OVF, bool PRE0 = false>
+template <bool COUNT, bool OVF, bool PRE0 = false, bool DQ = false>
 __device__ __forceinline__ int wide_node(float4 g0, float4 g1, float4 g2, float4 g3, FastRay& R, const LaneStack& st,
                                          Cnt& c, bool on = true, float tn0 = 0.0f, bool hit0 = false) {   // on = false: no child is hit
     const float cull = R.bk * CULL_MARGIN;
@@ -1245,14 +1257,30 @@ __device__ __forceinline__ int wide_node(float4 g0, float4 g1, float4 g2, float4
     int r[4] = {__float_as_int(g1.x), __float_as_int(g1.y), __float_as_int(g1.z), __float_as_int(g1.w)};
     float t[4];
     if (PRE0) t[0] = (on && r[0] != INT_MIN && hit0) ? tn0 : INFINITY;
+    // DQ (origin-folded): p - o once per node and axis, then each bound as fma(q, s, p - o) -- one
+    // subtract per bound fewer.  It rounds differently from (p + q s) - o, so it is conservative only
+    // because the builder keeps every bound with q > 0 at least 2^-17 P outside its child's exact
+    // bound (rt_api.hip emit_wide), which exceeds the rounding of the two forms, 2^-24 (|p - o| +
+    // |p + q s - o| + |b - o|) for a leaf bound b below, for every ray origin up to DevScene::wdq_omax
+    // (~20 P): a child box never rejects what a leaf below it accepts; q = 0 is fl(p - o) in both
+    // forms.  launch_fast picks DQ per frame (hit points are within P; the camera is checked).
+    const float px = g0.x - R.o.x, py = g0.y - R.o.y, pz = g0.z - R.o.z;
 #pragma unroll
     for (int i = PRE0 ? 1 : 0; i < 4; ++i) {
         // p + q * s with q * s exact (s a power of two, q < 256): one correctly rounded fma gives the
         // builder's p + (q * s) bit for bit
         auto dq = [&](float pp, unsigned w, float sc) { return fmaf((float)((w >> (8 * i)) & 255u), sc, pp); };
         float tn, tx;
-        slab(dq(g0.x, qlx, sx), dq(g0.x, qhx, sx), dq(g0.y, qly, sy), dq(g0.y, qhy, sy), dq(g0.z, qlz, sz),
-             dq(g0.z, qhz, sz), R.o, R.ix, R.iy, R.iz, tn, tx);
+        if (DQ) {
+            const float x0 = dq(px, qlx, sx) * R.ix, x1 = dq(px, qhx, sx) * R.ix;
+            const float y0 = dq(py, qly, sy) * R.iy, y1 = dq(py, qhy, sy) * R.iy;
+            const float z0 = dq(pz, qlz, sz) * R.iz, z1 = dq(pz, qhz, sz) * R.iz;
+            tn = fmaxf(fmaxf(fminf(x0, x1), fminf(y0, y1)), fminf(z0, z1));
+            tx = fminf(fminf(fmaxf(x0, x1), fmaxf(y0, y1)), fmaxf(z0, z1));
+        } else {
+            slab(dq(g0.x, qlx, sx), dq(g0.x, qhx, sx), dq(g0.y, qly, sy), dq(g0.y, qhy, sy), dq(g0.z, qlz, sz),
+                 dq(g0.z, qhz, sz), R.o, R.ix, R.iy, R.iz, tn, tx);
+        }
         t[i] = (on && r[i] != INT_MIN && box_hit(tn, tx, cull)) ? tn : INFINITY;   // misses sort last
     }
     if (COUNT && on) {
@@ -1313,7 +1341,7 @@ __device__ __forceinline__ bool wide_leaf(float4 g0, float4 g1, float4 g2, float
 // intersected.  Nodes and leaves are both 64 bytes, fetched with the same four 16-byte loads, like
 // fast_step.  The accepted triangles are the binary walk's (own exact leaf box passes, MT hit,
 // k > 1e-4, lowest (k, rank)), so the hit is the same.  Returns true when the ray is finished.
-template <bool COUNT, bool OVF>
+template <bool COUNT, bool OVF, bool DQ = false>
 __device__ __forceinline__ bool wide_step(FastRay& R, const char* nb, const char* lb, const LaneStack& st, Cnt& c) {
     const bool node = R.item >= 0;
     const char* p = node ? nb + 64u * (unsigned)R.item : lb + ~(unsigned)R.item;
@@ -1335,7 +1363,7 @@ __device__ __forceinline__ bool wide_step(FastRay& R, const char* nb, const char
          node ? dq0(g0.y, g3.x, 8) : g1.x, node ? dq0(g0.z, g2.z, 16) : g0.z, node ? dq0(g0.z, g3.y, 16) : g1.y, R.o,
          R.ix, R.iy, R.iz, tn0, tx0);
     const bool h0 = box_hit(tn0, tx0, R.bk * CULL_MARGIN);
-    const int nx = wide_node<COUNT, OVF, true>(g0, g1, g2, g3, R, st, c, node, tn0, h0);
+    const int nx = wide_node<COUNT, OVF, true, DQ>(g0, g1, g2, g3, R, st, c, node, tn0, h0);
     if (wide_leaf<COUNT, true>(g0, g1, g2, g3, R, c, !node, h0)) return true;
     if (nx != INT_MIN) {
         R.item = nx;

@@ -56,6 +56,10 @@ struct DevScene {
     const float4* wnodes;
     const float4* wleaves;
     int32_t wroot_ref;
+    // every quantised child bound with q > 0 lies 2^-17 P outside its exact bound (rt_api.hip emit_wide),
+    // which makes the origin-folded dequantisation conservative for ray origins with |o| <= wdq_omax
+    // (about 20 P; 0: no gap, exact form only); launch_fast checks the camera against it per frame
+    float wdq_omax;
     float root_box[6];     // min.xyz, max.xyz of the root
     // REF traversal: the reference's own AoS export, 9 floats per node
     const float* bvh9;
@@ -121,6 +125,7 @@ struct FrameParams {
     // anything (Raytracing.cl:125-137), so its traversal ends at the first accepted triangle
     int32_t sun_any;
     int32_t wide;        // FAST tree walk over the 4-wide quantised layout (DevScene::wnodes)
+    int32_t wdq;         // ... with origin-folded dequantisation when DevScene::wdq_omax covers the camera (1, default)
     // a sample that draws no random number (it ends at its first loop head: camera ray escaped or
     // on an emitter) is every later sample of its pixel: the rest are summed without re-running it
     int32_t fixed_point;

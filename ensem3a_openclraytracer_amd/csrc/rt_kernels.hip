@@ -371,7 +371,9 @@ constexpr size_t kStepMaxBytes = 16u << 20;
 // F.walk_team_dev (pass 2 of a pilot launch): the team size was chosen on the device from the pixels
 // pass 1 left unfinished (pilot_team_pick_kernel); the instantiations of the other sizes, launched
 // beside this one, return at once.
-template <bool COUNT, bool LOG, bool SMEM, bool OVF, bool STEP, bool WIDE, int TS = 1>
+// WIDE: 0 = the BVH2 walk, 1 = the 4-wide walk, 2 = the 4-wide walk with origin-folded dequantisation
+// (wide_node DQ; launch_fast picks it when the camera lies within DevScene::wdq_omax)
+template <bool COUNT, bool LOG, bool SMEM, bool OVF, bool STEP, int WIDE, int TS = 1>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WIDE ? kWideWaves : 4))) render_resume_kernel(DevScene S, FrameParams F, float* __restrict__ out,
                                                       unsigned long long* __restrict__ counts,
                                                       unsigned int* __restrict__ work_counter,
@@ -772,7 +774,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WIDE ?
         while (true) {
             if (tracing && (PIPE ? fast_step_pipe<COUNT, SMEM, OVF>(T, D, nb, tb, lst, kstride, c)
                             : TS > 1 ? team_step<COUNT, SMEM, OVF>(TS, T, boff, nb, tb, lst, kstride, c)
-                            : WIDE ? (STEP ? wide_step<COUNT, OVF>(T, wnb, wlb, lst, c)
+                            : WIDE ? (STEP ? wide_step<COUNT, OVF, WIDE == 2>(T, wnb, wlb, lst, c)
                                            : wide_round<COUNT, OVF>(T, wnb, wlb, lst, c))
                             : STEP ? fast_step<COUNT, SMEM, OVF>(S, T, nb, tb, lst, kstride, c)
                                    : fast_round<COUNT, SMEM, OVF>(S, T, nb, tb, lst, kstride, c)))
@@ -865,7 +867,7 @@ __global__ void pilot_team_pick_kernel(const unsigned* __restrict__ left, int64_
 }
 
 template <int TRAV, bool COUNT, bool LOG, bool SMEM = false, bool RESUME = false, bool OVF = false,
-          bool BRUTE = false, bool STEP = true, bool WIDE = false>
+          bool BRUTE = false, bool STEP = true, int WIDE = 0>
 hipError_t launch_t(const DevScene& sc, const FrameParams& fp, int block, float* d_out, unsigned long long* d_counts,
                     unsigned int* d_work, hipStream_t stream) {
     // FAST: int2 entries; the brute-force path of small scenes needs no stack
@@ -1005,6 +1007,7 @@ __global__ void debug_math_kernel(int fn, const float* __restrict__ x, const flo
         case 5: r = rtm_atan2(x[i], y[i]); break;
         case 6: r = sqrtf(x[i]); break;
         case 7: r = x[i] / y[i]; break;
+        case 8: r = mt_recip(x[i]); break;   // the Moller-Trumbore reciprocal of the FAST walks
         default: break;
     }
     out[i] = r;
@@ -1096,17 +1099,25 @@ hipError_t launch_fast(const DevScene& sc, const FrameParams& fp, int block, flo
     const bool resume = sc.ntri > 0 && sc.nbrute == 0 && fp.resume_min > 0;
     const bool step = fp.step == 1 || (fp.step == 0 && (size_t)sc.nnodes * kNodeF4 * 16 <= kStepMaxBytes);
     if (resume && fp.wide && sc.wnodes && !smem) {
-        // the wide walk takes item steps unless rounds are asked for (C5: 1,181 vs 1,035 Msamples/s)
+        // the wide walk takes item steps unless rounds are asked for (C5: 1,181 vs 1,035 Msamples/s);
+        // the item steps dequantise origin-folded (WIDE 2) when every ray origin of the frame is within
+        // the bound the builder's gap covers: hit points always are, the camera is checked here
         const bool step = fp.step != 2;
+        const float cmax = std::max(std::fabs(fp.cam[0]), std::max(std::fabs(fp.cam[1]), std::fabs(fp.cam[2])));
+        const bool dq = fp.wdq != 0 && sc.wdq_omax > 0.0f && cmax <= sc.wdq_omax;
         if (ovf)
-            return step ? launch_t<TRAV_FAST, COUNT, false, false, true, true, false, true, true>(
-                              sc, fp, block, d_out, d_counts, d_work, stream)
-                        : launch_t<TRAV_FAST, COUNT, false, false, true, true, false, false, true>(
-                              sc, fp, block, d_out, d_counts, d_work, stream);
-        return step ? launch_t<TRAV_FAST, COUNT, false, false, true, false, false, true, true>(
-                          sc, fp, block, d_out, d_counts, d_work, stream)
-                    : launch_t<TRAV_FAST, COUNT, false, false, true, false, false, false, true>(
-                          sc, fp, block, d_out, d_counts, d_work, stream);
+            return !step ? launch_t<TRAV_FAST, COUNT, false, false, true, true, false, false, 1>(
+                               sc, fp, block, d_out, d_counts, d_work, stream)
+                   : dq  ? launch_t<TRAV_FAST, COUNT, false, false, true, true, false, true, 2>(
+                               sc, fp, block, d_out, d_counts, d_work, stream)
+                         : launch_t<TRAV_FAST, COUNT, false, false, true, true, false, true, 1>(
+                               sc, fp, block, d_out, d_counts, d_work, stream);
+        return !step ? launch_t<TRAV_FAST, COUNT, false, false, true, false, false, false, 1>(
+                           sc, fp, block, d_out, d_counts, d_work, stream)
+               : dq  ? launch_t<TRAV_FAST, COUNT, false, false, true, false, false, true, 2>(
+                           sc, fp, block, d_out, d_counts, d_work, stream)
+                     : launch_t<TRAV_FAST, COUNT, false, false, true, false, false, true, 1>(
+                           sc, fp, block, d_out, d_counts, d_work, stream);
     }
     if (resume) {
         return step ? launch_resume<COUNT, true>(sc, fp, block, d_out, d_counts, d_work, stream, smem, ovf)

@@ -92,7 +92,10 @@ int rt_set_env(rt_ctx* ctx, const uint8_t* rgba, int w, int h);
  * frame), "slices" (one-pass tree-walk launches: each pixel's samples as K
  * jobs handed out slice-major, 0 = off, -1 = auto: 8 on the 4-wide walk --
  * same frame), "handout" (1 = a contiguous pixel block per XCD group, 0 =
- * interleaved chunks, -1 = auto: 1 on the 4-wide walk), "waves" (persistent
+ * interleaved chunks, -1 = auto: 1 on the 4-wide walk), "wdq" (4-wide walk:
+ * 1 = child boxes dequantised origin-folded where the layout's quantisation gap
+ * covers the frame's camera, 0 = always the (p + q s) - o form -- same frame),
+ * "waves" (persistent
  * grid: at most this many waves per SIMD, 0 = occupancy limit), "block"
  * (threads per block: 64, 128 or 256), and the tuning switches documented in
  * DESIGN.md 4.2 ("sun_skip", "sun_any", "fixed_point", "sun_cache", "pilot",

@@ -13,7 +13,8 @@ extern "C" {
 
 /* Evaluate a function of the numerics contract (rtm.h) on device 0 over host
  * arrays: fn 0 sin, 1 cos, 2 tan, 3 asin, 4 acos, 5 atan2(x, y), 6 sqrt,
- * 7 x / y.  y may be NULL for unary functions. */
+ * 7 x / y, 8 the FAST walks' Moller-Trumbore reciprocal of x (rt_device.h mt_recip: equal to
+ * 1.0f / x for 1e-7 <= |x| <= 2^126 and for infinities and NaN).  y may be NULL for unary functions. */
 int rt_debug_math(rt_ctx* ctx, int fn, const float* x, const float* y, float* out, int64_t n);
 
 /* Trace n rays (rays[6*i..] = dir.xyz, origin.xyz) through the uploaded
@@ -39,15 +40,18 @@ int rt_debug_wave_counts(rt_ctx* ctx, const float cam[10], const float env[5], i
 /* Scene facts: out[0] = FAST layout available (1/0), out[1] = FAST stack
  * depth, out[2] = internal nodes, out[3] = triangles, out[4] = brute-force
  * records (0: the tree walk renders), out[5] = distinct leaf boxes of the
- * brute-force path, out[6], out[7] = 0. */
+ * brute-force path, out[6] = the largest camera coordinate magnitude for which
+ * the 4-wide walk dequantises origin-folded, in millionths (0: never), out[7] = 0. */
 int rt_debug_scene_info(rt_ctx* ctx, int64_t out[8]);
 
 /* Host-only (no device): the per-axis quantisation of the 4-wide layout (rt_api.hip emit_wide).
  * For up to n = 4 child intervals [lo[c], hi[c]] against the lower corner p, returns the biased
  * exponent byte e (scale 2^(e-127)) and byte bounds with p + qlo[c] * 2^(e-127) <= lo[c] and
- * p + qhi[c] * 2^(e-127) >= hi[c] in fp32, or -1 when no scale up to 2^100 contains every interval
- * (non-finite bounds, extents beyond 255 * 2^100): the scene then keeps the BVH2 walk. */
-int rt_debug_quantise_axis(float p, const float* lo, const float* hi, int n, uint8_t* qlo, uint8_t* qhi);
+ * p + qhi[c] * 2^(e-127) >= hi[c] in fp32 and, for every byte q > 0, at least `gap` outside the
+ * interval in exact arithmetic (p + qlo s <= lo - gap, p + qhi s >= hi + gap; gap >= 0), or -1 when
+ * no scale up to 2^100 does (non-finite bounds, extents beyond 255 * 2^100): the scene then keeps the
+ * BVH2 walk (gap = 0) or quantises without the gap (emit_wide). */
+int rt_debug_quantise_axis(float p, const float* lo, const float* hi, int n, float gap, uint8_t* qlo, uint8_t* qhi);
 
 #ifdef __cplusplus
 }

@@ -60,6 +60,27 @@ def test_device_numerics_bit_identical(kl):
         assert same.all(), (name, x[~same][:5], g[~same][:5], c[~same][:5])
 
 
+def test_mt_reciprocal_is_the_ieee_division(kl):
+    """mt_recip (rt_device.h: v_rcp_f32, one fma Newton step, v_div_fixup) is the FAST walks' 1/a: it
+    must equal the IEEE 1.0f / a wherever Moller-Trumbore uses it -- |a| >= 1e-7 (smaller is the
+    parallel case), up to 2^126 (pack_fast keeps scenes below it), and infinities / NaN.  Exhaustive
+    over all 2^32 inputs in profiles/r05_rcp_exhaustive.json (tools/rcp_exhaustive.hip); here every
+    4099th bit pattern plus the edges."""
+    bits = np.arange(0, 1 << 32, 4099, dtype=np.uint64).astype(np.uint32)
+    edge = np.array([0x33D6BF95, 0x33D6BF96, 0x7E7FFFFF, 0x7E800000, 0x7F7FFFFF, 0x7F800000, 0x7FC00000,
+                     0x00800000, 0x3F800000, 0x3F7FFFFF, 0x3F800001], np.uint32)
+    bits = np.concatenate([bits, edge, edge | np.uint32(0x80000000)])
+    x = bits.view(np.float32)
+    with np.errstate(divide="ignore", over="ignore", invalid="ignore"):
+        want = np.float32(1.0) / x
+    got = kl.native.debug_math(8, x)
+    ax = np.abs(x)
+    used = (ax >= np.float32(1e-7)) & (ax <= np.float32(2.0 ** 126)) | np.isinf(x) | np.isnan(x)
+    same = (got.view(np.uint32) == want.view(np.uint32)) | (np.isnan(got) & np.isnan(want))
+    assert used.sum() > 500000
+    assert same[used].all(), (x[used & ~same][:5], got[used & ~same][:5], want[used & ~same][:5])
+
+
 @pytest.mark.parametrize("case", list(W.PARITY_CASES))
 def test_ref_traversal_bit_identical_to_oracle(kl, case):
     sc, cam, env, npix, spp, mb, ibl = W.PARITY_CASES[case].inputs()
@@ -944,6 +965,40 @@ def test_wide_layout_renders_identically(kl, case):
     with pytest.raises(_native.NativeError, match="bvh_width"):
         kl.native.set_option("bvh_width", 8)
 
+
+
+@pytest.mark.parametrize("case", ["grid", "monkey_c3_64_s4", "serre_96x54_s4", "furnace_64_s4"])
+def test_wide_origin_folded_dequantisation_renders_identically(kl, case):
+    """wdq: the 4-wide walk's child boxes dequantised as fma(q, s, p - o) instead of (p + q s) - o.  It
+    rounds differently; the builder keeps every bound with q > 0 at least 2^-17 P outside its exact
+    bound, which covers both roundings for ray origins up to scene_info's wdq_omax (rt_api.hip
+    emit_wide), so the accepted triangles -- and the frame -- are the exact form's and the oracle's.  A
+    camera beyond the bound renders with the exact form (launch_fast), the same frame again."""
+    if case == "grid":
+        sc, cam, env, npix, spp, mb, ibl = W.CONFIGS["C5"].with_size(48, 27, 2).inputs()
+    else:
+        sc, cam, env, npix, spp, mb, ibl = W.PARITY_CASES[case].inputs()
+    try:
+        kl.native.set_option("bvh_width", 4)
+        dq = _launch(kl, sc, cam, env, npix, spp, mb, ibl, "fast")
+        omax = kl.native.scene_info()["wdq_omax"]
+        kl.native.set_option("wdq", 0)
+        exact = _launch(kl, sc, cam, env, npix, spp, mb, ibl, "fast")
+        far = np.array(cam, np.float32).copy()
+        far[:3] = far[:3] + np.float32(2.0 * omax + 1.0)   # beyond the bound: the exact form either way
+        kl.native.set_option("wdq", 1)
+        far_dq = _launch(kl, sc, far, env, npix, spp, mb, ibl, "fast")
+        kl.native.set_option("wdq", 0)
+        far_exact = _launch(kl, sc, far, env, npix, spp, mb, ibl, "fast")
+    finally:
+        kl.native.set_option("bvh_width", 0)
+        kl.native.set_option("wdq", 1)
+    assert omax > float(np.abs(np.asarray(cam[:3], np.float64)).max()), "the camera should be within the bound"
+    np.testing.assert_array_equal(dq, exact)
+    np.testing.assert_array_equal(dq, _oracle(sc, cam, env, npix, spp, mb, ibl))
+    np.testing.assert_array_equal(far_dq, far_exact)
+    with pytest.raises(_native.NativeError, match="wdq"):
+        kl.native.set_option("wdq", 2)
 
 
 @pytest.mark.parametrize("case", ["serre_96x54_s4", "cornell_128_s16", "monkey_c3_64_s4", "serre_sky_s64"])

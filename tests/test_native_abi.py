@@ -59,22 +59,26 @@ def test_bvh_through_abi_validates():
         build_export_array(np.array([0] * 7 + [5, 6, 7], np.int32), np.zeros(9, np.float32))
 
 
-def _quantise(p, lo, hi):
+def _quantise(p, lo, hi, gap=0.0):
     lib = ctypes.CDLL(LIB)
     f = lib.rt_debug_quantise_axis
     f.restype = ctypes.c_int
-    f.argtypes = [ctypes.c_float, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
+    f.argtypes = [ctypes.c_float, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_float, ctypes.c_void_p,
+                  ctypes.c_void_p]
     lo = np.ascontiguousarray(lo, np.float32)
     hi = np.ascontiguousarray(hi, np.float32)
     ql = np.zeros(4, np.uint8)
     qh = np.zeros(4, np.uint8)
-    e = f(np.float32(p), lo.ctypes.data, hi.ctypes.data, len(lo), ql.ctypes.data, qh.ctypes.data)
+    e = f(np.float32(p), lo.ctypes.data, hi.ctypes.data, len(lo), np.float32(gap), ql.ctypes.data, qh.ctypes.data)
     return e, ql[:len(lo)], qh[:len(lo)]
 
 
-def test_wide_quantisation_contains_every_child_box():
+@pytest.mark.parametrize("rel_gap", [0.0, 2.0 ** -17])
+def test_wide_quantisation_contains_every_child_box(rel_gap):
     """The 4-wide layout's byte bounds dequantise (p + q * 2^(e-127), fp32) to a superset of each
-    child interval, so an ancestor never culls what a leaf accepts (rt_api.hip emit_wide)."""
+    child interval, so an ancestor never culls what a leaf accepts (rt_api.hip emit_wide); with a gap
+    (emit_wide: 2^-17 of the scene's largest coordinate) every bound with q > 0 also lies at least the
+    gap outside, in exact arithmetic, which the origin-folded dequantisation relies on."""
     rng = np.random.default_rng(5)
     for _ in range(300):
         n = int(rng.integers(1, 5))
@@ -82,12 +86,17 @@ def test_wide_quantisation_contains_every_child_box():
         lo = (rng.standard_normal(n) * scale).astype(np.float32)
         hi = (lo + np.abs(rng.standard_normal(n)) * scale).astype(np.float32)
         p = np.float32(lo.min())
-        e, ql, qh = _quantise(p, lo, hi)
+        gap = np.float32(rel_gap * float(np.abs(np.concatenate([lo, hi])).max()))
+        e, ql, qh = _quantise(p, lo, hi, gap)
         assert 0 <= e <= 227
         s = np.float32(2.0 ** (e - 127))
         dlo = (p + ql.astype(np.float32) * s).astype(np.float32)
         dhi = (p + qh.astype(np.float32) * s).astype(np.float32)
         assert np.all(dlo <= lo) and np.all(dhi >= hi)
+        xlo = float(p) + ql.astype(np.float64) * float(s)   # exact: p and q s are floats, q < 256
+        xhi = float(p) + qh.astype(np.float64) * float(s)
+        assert np.all((ql == 0) | (xlo <= lo.astype(np.float64) - float(gap)))
+        assert np.all((qh == 0) | (xhi >= hi.astype(np.float64) + float(gap)))
 
 
 @pytest.mark.parametrize("lo,hi", [
