@@ -779,6 +779,29 @@ def test_ref_stack_overflow_drops_like_the_reference(kl):
     ctx.close()
 
 
+def test_huge_triangles_render_with_the_reference_walk(kl):
+    """The FAST walks' Moller-Trumbore reciprocal (mt_recip) is the IEEE 1/a only up to |a| = 2^126, and
+    |a| <= |e1| |e2| for unit directions: a scene whose triangle edges could pass that (pack_checked:
+    |e1| |e2| > 2^120) is rendered by the REF walk -- the reference's own -- whatever "traversal" says,
+    bit for bit the oracle's frame."""
+    sc, cam, env, npix, spp, mb, ibl = W.PARITY_CASES["monkey_c3_64_s4"].inputs()
+    k = np.float32(2.0 ** 63)
+    vp = (np.asarray(sc.V_p, np.float32) * k).astype(np.float32)
+    bvh = np.asarray(sc.BVH.exportArray, np.float32).reshape(-1, 9).copy()
+    bvh[:, 2:8] *= k
+    bvh = bvh.reshape(-1)
+    cam = np.array(cam, np.float32).copy()
+    cam[:3] *= k
+    ctx = _native.Context(device_ids=[0])
+    ctx.set_scene(vp, sc.V_n, sc.V_uv, sc.faceData, sc.materialData, bvh)
+    ctx.set_env(ibl)
+    assert not ctx.scene_info()["fast_ok"]
+    got = ctx.render(cam, env, npix, spp, mb)
+    ctx.close()
+    osc = O.OracleScene(vp, sc.V_n, sc.V_uv, sc.faceData, sc.materialData, bvh, ibl)
+    np.testing.assert_array_equal(got, O.render(osc, cam, env, npix, spp, mb, nthreads=16))
+
+
 @pytest.mark.parametrize("config,row0,row_step", [("C3", 7, 64), ("C4", 3, 72)])
 def test_full_size_rows_match_oracle(kl, config, row0, row_step):
     """C3 (1024^2, 256 spp, glass + glossy) and C4 (1920x1080 top-anchored, 512 spp, 8k IBL) at
