@@ -215,7 +215,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) r
                         brdf = cm.color;
                         invPdf = 1.0f / rtm_fabs(rtm_dot(Bd, nn));
                     }
-                    const rtm_f3 nd = rtm_normalize(Rd);
+                    const rtm_f3 nd = dev_normalize(Rd);
                     Bo = rtm_v3(fmaf(nd.x, kh, Ro.x), fmaf(nd.y, kh, Ro.y), fmaf(nd.z, kh, Ro.z));
                     // attenuation depends only on pre-trace values (Raytracing.cl:86-87): apply now
                     const float att = invPdf * rtm_fabs(rtm_dot(Bd, nn));
@@ -743,7 +743,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WIDE ?
                             brdf = cm.color;
                             invPdf = 1.0f / rtm_fabs(rtm_dot(Bd, nn));
                         }
-                        const rtm_f3 nd = rtm_normalize(Rd);
+                        const rtm_f3 nd = dev_normalize(Rd);
                         const rtm_f3 Bo = rtm_v3(fmaf(nd.x, k, Ro.x), fmaf(nd.y, k, Ro.y), fmaf(nd.z, k, Ro.z));
                         // attenuation depends only on pre-trace values (Raytracing.cl:86-87): apply now
                         const float att = invPdf * rtm_fabs(rtm_dot(Bd, nn));
