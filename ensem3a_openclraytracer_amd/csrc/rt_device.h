@@ -194,11 +194,13 @@ __device__ __forceinline__ float dev_sqrt(float x) {
     if (__builtin_expect(!sqrt_fast_ok(x), 0)) r = sqrtf(x);
     return r;
 }
-__device__ __forceinline__ rtm_f3 dev_normalize(rtm_f3 v) {   // rtm_normalize, bit for bit
-    const float d = rtm_dot(v, v);
+__device__ __forceinline__ float dev_inv_sqrt(float d) {   // 1.0f / sqrtf(d), bit for bit
     float s = mt_recip(sqrt_rsq(d));
     if (__builtin_expect(!sqrt_fast_ok(d), 0)) s = 1.0f / sqrtf(d);
-    return rtm_scale(v, s);
+    return s;
+}
+__device__ __forceinline__ rtm_f3 dev_normalize(rtm_f3 v) {   // rtm_normalize, bit for bit
+    return rtm_scale(v, dev_inv_sqrt(rtm_dot(v, v)));
 }
 
 // Moller-Trumbore on a triangle given as (a.p, e1, e2): MathLib.cl:117-160's arithmetic.

@@ -1008,6 +1008,8 @@ __global__ void debug_math_kernel(int fn, const float* __restrict__ x, const flo
         case 6: r = sqrtf(x[i]); break;
         case 7: r = x[i] / y[i]; break;
         case 8: r = mt_recip(x[i]); break;   // the Moller-Trumbore reciprocal of the FAST walks
+        case 9: r = dev_sqrt(x[i]); break;   // the shading's sqrtf
+        case 10: r = dev_inv_sqrt(x[i]); break;   // dev_normalize's scale, 1.0f / sqrtf
         default: break;
     }
     out[i] = r;

@@ -81,6 +81,26 @@ def test_mt_reciprocal_is_the_ieee_division(kl):
     assert same[used].all(), (x[used & ~same][:5], got[used & ~same][:5], want[used & ~same][:5])
 
 
+def test_device_sqrt_and_inverse_sqrt_are_ieee(kl):
+    """dev_sqrt / dev_inv_sqrt (rt_device.h: v_rsq_f32 and one Newton step, then mt_recip; the IEEE
+    forms in a branch outside [2^-96, 2^126]) must be the IEEE sqrtf and 1.0f / sqrtf for every input:
+    every 4099th bit pattern plus the edges of the fast range (exhaustive over [2^-96, 2^126] in
+    profiles/r05_sqrt_exhaustive.json)."""
+    bits = np.arange(0, 1 << 32, 4099, dtype=np.uint64).astype(np.uint32)
+    edge = np.array([0x0F800000, 0x0F7FFFFF, 0x0F800001, 0x7E800000, 0x7E800001, 0x7E7FFFFF, 0x7F7FFFFF,
+                     0x7F800000, 0x7FC00000, 0x00000001, 0x00800000, 0x3F800000, 0x3F7FFFFF, 0],
+                    np.uint32)
+    bits = np.concatenate([bits, edge, edge | np.uint32(0x80000000)])
+    x = bits.view(np.float32)
+    with np.errstate(divide="ignore", invalid="ignore"):
+        sq = np.sqrt(x)
+        inv = np.float32(1.0) / sq
+    for fn, want in ((9, sq), (10, inv)):
+        got = kl.native.debug_math(fn, x)
+        same = (got.view(np.uint32) == want.view(np.uint32)) | (np.isnan(got) & np.isnan(want))
+        assert same.all(), (fn, x[~same][:5], got[~same][:5], want[~same][:5])
+
+
 @pytest.mark.parametrize("case", list(W.PARITY_CASES))
 def test_ref_traversal_bit_identical_to_oracle(kl, case):
     sc, cam, env, npix, spp, mb, ibl = W.PARITY_CASES[case].inputs()
