@@ -177,6 +177,15 @@ __device__ __forceinline__ float mt_recip(float a) {
     return __builtin_amdgcn_div_fixupf(fmaf(e, r, r), a, 1.0f);
 }
 
+// 1.0f / x for any x: mt_recip where it is the IEEE result (1e-7 <= |x| <= 2^126, profiles/
+// r05_rcp_exhaustive.json), the IEEE division in a branch no lane normally takes otherwise
+__device__ __forceinline__ float dev_recip(float x) {
+    const float ax = fabsf(x);
+    float r = mt_recip(x);
+    if (__builtin_expect(!(ax >= 0.0000001f && ax <= 0x1p126f), 0)) r = 1.0f / x;
+    return r;
+}
+
 // sqrtf(x) and 1.0f / sqrtf(x) (rtm_normalize's scale) in 5 and 9 instructions instead of ~16 and ~27:
 // the v_rsq_f32 seed with one Newton step, then mt_recip, are bit-identical to the IEEE sqrtf and to
 // 1.0f / sqrtf for every x in [2^-96, 2^126] -- checked on the MI355X over all 2^32 inputs
@@ -335,7 +344,7 @@ __device__ Hit trace_fast(const DevScene& S, const float4* __restrict__ nodes, c
     // AoS: node i = 64 bytes at 64 i; SOA (LDS copy): plane k of node i at 16 (k nnodes + i), so
     // 16 lanes reading 16 different nodes hit 16 different bank groups
     const unsigned kstride = SOA ? 16u * (unsigned)S.nnodes : 16u;
-    const float ix = 1.0f / d.x, iy = 1.0f / d.y, iz = 1.0f / d.z;
+    const float ix = dev_recip(d.x), iy = dev_recip(d.y), iz = dev_recip(d.z);
     float tmin, tmax;
     slab(S.root_box[0], S.root_box[3], S.root_box[1], S.root_box[4], S.root_box[2], S.root_box[5], o, ix, iy, iz,
          tmin, tmax);
@@ -455,7 +464,7 @@ __device__ Hit trace_brute_compact(const DevScene& S, rtm_f3 o, rtm_f3 d, char* 
     const unsigned long long nokey = ((unsigned long long)__float_as_uint(1000.0f) << 32) | 0xffffffffull;
     bestk[lane] = nokey;
     wave_lds_sync();
-    const float ix = 1.0f / d.x, iy = 1.0f / d.y, iz = 1.0f / d.z;
+    const float ix = dev_recip(d.x), iy = dev_recip(d.y), iz = dev_recip(d.z);
     float bk = 1000.0f;
     unsigned head = 0, tail = 0;   // wave-uniform ring positions
     auto run_batch = [&](int n) __attribute__((always_inline)) {
@@ -785,7 +794,7 @@ __device__ __forceinline__ rtm_f3 brdf_ggx(rtm_f3 color, float rough, rtm_f3 v, 
     const float p5 = (om2 * om2) * om;
     const float F = fmaf(1.0f - F0, p5, F0);
     const float spec = (F * G * D) *
-        (1.0f / rtm_fmax(4.0f * rtm_fmax(rtm_dot(v, n), 0.0f) * rtm_fmax(rtm_dot(l, n), 0.0f), 0.001f));
+        dev_recip(rtm_fmax(4.0f * rtm_fmax(rtm_dot(v, n), 0.0f) * rtm_fmax(rtm_dot(l, n), 0.0f), 0.001f));
     rtm_f3 kd = rtm_v3(1.0f - F, 1.0f - F, 1.0f - F);
     kd = rtm_scale(kd, 1.0f - 0.5f);
     const rtm_f3 diffuse = rtm_div(rtm_mul(kd, color), 3.14f);
@@ -956,9 +965,9 @@ __device__ __forceinline__ bool fast_init(const DevScene& S, FastRay& R, rtm_f3 
     R.brank = -1;
     R.soff = 0;
     if (S.ntri <= 0) return true;
-    R.ix = 1.0f / d.x;
-    R.iy = 1.0f / d.y;
-    R.iz = 1.0f / d.z;
+    R.ix = dev_recip(d.x);
+    R.iy = dev_recip(d.y);
+    R.iz = dev_recip(d.z);
     float tmin, tmax;
     slab(S.root_box[0], S.root_box[3], S.root_box[1], S.root_box[4], S.root_box[2], S.root_box[5], o, R.ix, R.iy, R.iz,
          tmin, tmax);

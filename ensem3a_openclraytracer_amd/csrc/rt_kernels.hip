@@ -1010,6 +1010,7 @@ __global__ void debug_math_kernel(int fn, const float* __restrict__ x, const flo
         case 8: r = mt_recip(x[i]); break;   // the Moller-Trumbore reciprocal of the FAST walks
         case 9: r = dev_sqrt(x[i]); break;   // the shading's sqrtf
         case 10: r = dev_inv_sqrt(x[i]); break;   // dev_normalize's scale, 1.0f / sqrtf
+        case 11: r = dev_recip(x[i]); break;   // the kernels' 1.0f / x (ray inverses, GGX)
         default: break;
     }
     out[i] = r;

@@ -15,8 +15,8 @@ extern "C" {
  * arrays: fn 0 sin, 1 cos, 2 tan, 3 asin, 4 acos, 5 atan2(x, y), 6 sqrt,
  * 7 x / y, 8 the FAST walks' Moller-Trumbore reciprocal of x (rt_device.h mt_recip: equal to
  * 1.0f / x for 1e-7 <= |x| <= 2^126 and for infinities and NaN), 9 the kernels' sqrtf, 10 their
- * 1.0f / sqrtf(x) (rt_device.h dev_sqrt / dev_inv_sqrt: the IEEE results for every x).  y may be NULL
- * for unary functions. */
+ * 1.0f / sqrtf(x) (rt_device.h dev_sqrt / dev_inv_sqrt: the IEEE results for every x), 11 their
+ * 1.0f / x (dev_recip, likewise).  y may be NULL for unary functions. */
 int rt_debug_math(rt_ctx* ctx, int fn, const float* x, const float* y, float* out, int64_t n);
 
 /* Trace n rays (rays[6*i..] = dir.xyz, origin.xyz) through the uploaded

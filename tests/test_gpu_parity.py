@@ -82,7 +82,7 @@ def test_mt_reciprocal_is_the_ieee_division(kl):
 
 
 def test_device_sqrt_and_inverse_sqrt_are_ieee(kl):
-    """dev_sqrt / dev_inv_sqrt (rt_device.h: v_rsq_f32 and one Newton step, then mt_recip; the IEEE
+    """dev_sqrt / dev_inv_sqrt / dev_recip (rt_device.h: v_rsq_f32 and one Newton step, then mt_recip; the IEEE
     forms in a branch outside [2^-96, 2^126]) must be the IEEE sqrtf and 1.0f / sqrtf for every input:
     every 4099th bit pattern plus the edges of the fast range (exhaustive over [2^-96, 2^126] in
     profiles/r05_sqrt_exhaustive.json)."""
@@ -92,10 +92,11 @@ def test_device_sqrt_and_inverse_sqrt_are_ieee(kl):
                     np.uint32)
     bits = np.concatenate([bits, edge, edge | np.uint32(0x80000000)])
     x = bits.view(np.float32)
-    with np.errstate(divide="ignore", invalid="ignore"):
+    with np.errstate(divide="ignore", invalid="ignore", over="ignore"):
         sq = np.sqrt(x)
         inv = np.float32(1.0) / sq
-    for fn, want in ((9, sq), (10, inv)):
+        rec = np.float32(1.0) / x
+    for fn, want in ((9, sq), (10, inv), (11, rec)):
         got = kl.native.debug_math(fn, x)
         same = (got.view(np.uint32) == want.view(np.uint32)) | (np.isnan(got) & np.isnan(want))
         assert same.all(), (fn, x[~same][:5], got[~same][:5], want[~same][:5])
