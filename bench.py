@@ -30,7 +30,7 @@ Extra fields (DESIGN.md 5 derives every number):
                    (SQ_INSTS_VALU x 64) per launch, when committed.
   host_boundary -- rt_render (launch_Raytracing's blocking C-ABI: kernel + copy of
                    the frame into caller memory), timed over the same W/K steps.
-  configs       -- C1 (20 steps), C3, C4 and C5 (2 steps, 1 warmup) timed the same way (per-frame min / median
+  configs       -- C1 (20 steps), C3 and C4 (5 steps) and C5 (2 steps), 1+ warmup, timed the same way (per-frame min / median
                    and the GPU clock beside them); at N=1 on one device (with their roofline and the CPU
                    oracle's rate: C1 whole frame, C3-C5 per sample at 16 spp), at N>1 through the same
                    row tiles + RCCL gather as the headline (every config's strong scaling).
@@ -566,7 +566,8 @@ def main():
             ctx = None
             cpu = not args.no_cpu_baseline
             line["configs"] = {"C1": time_config(make_ctx, "C1", 20, 3, cpu)}
-            line["configs"].update({c: time_config(make_ctx, c, 2, 1, cpu) for c in ("C3", "C4", "C5")})
+            # C3 / C4 over 5 frames (about 0.5 / 1.4 s: their frames spread 1-3 % within a run), C5 over 2
+            line["configs"].update({c: time_config(make_ctx, c, st, 1, cpu) for c, st in (("C3", 5), ("C4", 5), ("C5", 2))})
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(wl, scene, ibl, cam, env)
         print(json.dumps(line), flush=True)
