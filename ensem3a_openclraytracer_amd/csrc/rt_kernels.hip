@@ -213,7 +213,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) r
                     } else {
                         Bd = Rd;
                         brdf = cm.color;
-                        invPdf = dev_recip(rtm_fabs(rtm_dot(Bd, nn)));
+                        invPdf = 1.0f / rtm_fabs(rtm_dot(Bd, nn));
                     }
                     const rtm_f3 nd = dev_normalize(Rd);
                     Bo = rtm_v3(fmaf(nd.x, kh, Ro.x), fmaf(nd.y, kh, Ro.y), fmaf(nd.z, kh, Ro.z));
@@ -741,7 +741,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WIDE ?
                         } else {
                             Bd = Rd;
                             brdf = cm.color;
-                            invPdf = dev_recip(rtm_fabs(rtm_dot(Bd, nn)));
+                            invPdf = 1.0f / rtm_fabs(rtm_dot(Bd, nn));
                         }
                         const rtm_f3 nd = dev_normalize(Rd);
                         const rtm_f3 Bo = rtm_v3(fmaf(nd.x, k, Ro.x), fmaf(nd.y, k, Ro.y), fmaf(nd.z, k, Ro.z));

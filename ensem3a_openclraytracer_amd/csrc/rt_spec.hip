@@ -410,7 +410,7 @@ spec_kernel(DevScene S, FrameParams F, float* __restrict__ out, unsigned int* __
                         } else {
                             Bd = Rd;
                             brdf = cm.color;
-                            invPdf = dev_recip(rtm_fabs(rtm_dot(Bd, nn)));
+                            invPdf = 1.0f / rtm_fabs(rtm_dot(Bd, nn));
                         }
                         const rtm_f3 nd = dev_normalize(Rd);
                         const rtm_f3 Bo = rtm_v3(fmaf(nd.x, k, Ro.x), fmaf(nd.y, k, Ro.y), fmaf(nd.z, k, Ro.z));
