@@ -18,8 +18,8 @@ LIBDIR = os.path.join(PKG, "lib")
 LIB = os.path.join(LIBDIR, "libensem3a_rt.so")
 OBJDIR = os.path.join(ROOT, "build", "native")
 
-SOURCES = ["rt_kernels.hip", "rt_spec.hip", "rt_api.hip", "bvh_build.cpp", "bvh_sah.cpp", "obj_load.cpp"]
-HEADERS = ["rt_internal.h", "rt_device.h", "rtm.h", "bvh_sah.h"]
+SOURCES = ["rt_kernels.hip", "rt_spec.hip", "rt_api.hip", "scene_pack.cpp", "bvh_build.cpp", "bvh_sah.cpp", "obj_load.cpp"]
+HEADERS = ["rt_internal.h", "rt_layout.h", "scene_pack.h", "rt_device.h", "rtm.h", "bvh_sah.h"]
 # -ffp-contract=off: the numerics contract (rtm.h) places every fused multiply-add explicitly.
 COMMON = ["-O3", "-std=c++17", "-ffp-contract=off", "-fno-fast-math", "-fno-slp-vectorize", "-fPIC", "-Wall",
           "-Wno-unused-function", "-I", os.path.join(ROOT, "include")]

@@ -15,6 +15,7 @@ from ._build import LIB
 
 _lock = threading.Lock()
 _lib = None
+_host = None
 
 RT_TRAVERSAL_FAST = 0
 RT_TRAVERSAL_REF = 1
@@ -27,9 +28,14 @@ EXPORTED = (
     "rt_render", "rt_render_device", "rt_tile_rows", "rt_count_work", "rt_count_work_detail", "rt_work_bytes", "rt_gamma",
     "rt_render_rgb8", "rt_rgb8_device", "rt_rgb8",
     "rt_bvh_build", "rt_device_count", "rt_debug_math", "rt_debug_trace", "rt_debug_scene_info", "rt_debug_pixel_log",
-    "rt_debug_wave_counts", "rt_debug_quantise_axis",
+    "rt_debug_wave_counts", "rt_debug_quantise_axis", "rt_debug_timings",
     "rt_obj_parse", "rt_obj_size", "rt_obj_copy", "rt_obj_free", "rt_obj_last_error",
+    "rt_scene_check", "rt_scene_last_error",
 )
+# The host-only entry points (no GPU, no HIP call): the sanitizer build (oracle/Makefile asan,
+# tools/sanitize.sh) compiles exactly these into an ASan/UBSan library that ENSEM3A_HOST_LIB selects.
+HOST_ONLY = ("rt_bvh_build", "rt_obj_parse", "rt_obj_size", "rt_obj_copy", "rt_obj_free", "rt_obj_last_error",
+             "rt_scene_check", "rt_scene_last_error", "rt_debug_quantise_axis")
 
 _c_p = ctypes.c_void_p
 _i64 = ctypes.c_int64
@@ -102,18 +108,51 @@ def lib():
             "rt_obj_copy": (_i32, [_c_p, _c_p, _c_p, _c_p, _c_p]),
             "rt_obj_free": (None, [_c_p]),
             "rt_obj_last_error": (ctypes.c_char_p, []),
+            "rt_scene_check": (_i32, [_c_p, _i64, _c_p, _i64, _c_p, _i64, _c_p, _i64, _c_p, _i64, _i32, _c_p]),
+            "rt_scene_last_error": (ctypes.c_char_p, []),
             "rt_debug_math": (_i32, [_c_p, _i32, _c_p, _c_p, _c_p, _i64]),
             "rt_debug_trace": (_i32, [_c_p, _i32, _c_p, _c_p, _i64]),
             "rt_debug_scene_info": (_i32, [_c_p, _c_p]),
+            "rt_debug_timings": (_i32, [_c_p, _c_p]),
             "rt_debug_wave_counts": (_i32, [_c_p, _c_p, _c_p, _i64, _i32, _i32, _c_p]),
             "rt_debug_pixel_log": (_i32, [_c_p, _i32, _c_p, _c_p, _i64, _i32, _i32, _i64, _c_p, _i32, _c_p, _c_p]),
         }
-        for name, (res, args) in sig.items():
-            fn = getattr(L, name)
-            fn.restype = res
-            fn.argtypes = args
+        _bind(L, sig)
         _lib = L
     return _lib
+
+
+_HOST_SIG = {}
+
+
+def _bind(L, sig, names=None):
+    for name, (res, args) in sig.items():
+        if names is not None and name not in names:
+            continue
+        fn = getattr(L, name)
+        fn.restype = res
+        fn.argtypes = args
+        if name in HOST_ONLY:
+            _HOST_SIG[name] = (res, args)
+
+
+def host_lib():
+    """The library serving the host-only entry points (HOST_ONLY): the product library, or the
+    sanitizer build named by ENSEM3A_HOST_LIB (tools/sanitize.sh)."""
+    global _host
+    if _host is not None:
+        return _host
+    L = lib()
+    path = os.environ.get("ENSEM3A_HOST_LIB")
+    if path:
+        with _lock:
+            if _host is None:
+                H = ctypes.CDLL(path)
+                _bind(H, _HOST_SIG)
+                _host = H
+        return _host
+    _host = L
+    return _host
 
 
 def check(status: int, ctx=None) -> None:
@@ -302,22 +341,46 @@ class Context:
         return dict(fast_ok=bool(out[0]), depth=int(out[1]), nodes=int(out[2]), tris=int(out[3]),
                     brute_records=int(out[4]), brute_boxes=int(out[5]), wdq_omax=int(out[6]) * 1e-6)
 
+    def timings(self) -> dict:
+        """Host wall times (ms) of the last set_scene (pack / upload), set_env and render (rt_debug_timings)."""
+        out = np.zeros(4, dtype=np.float64)
+        self._check(lib().rt_debug_timings(self.handle, out.ctypes.data))
+        return dict(pack_ms=float(out[0]), upload_ms=float(out[1]), env_ms=float(out[2]), render_ms=float(out[3]))
+
 
 def parse_obj(text):
     """Native OBJ import (include/rt_scene.h): ``(V_p, V_n, V_uv, faceData, matCounter)``
     with the reference importer's semantics (FileManager.py:253-304).  Host only."""
     data = text.encode() if isinstance(text, str) else bytes(text)
     h = _c_p()
-    if lib().rt_obj_parse(data, len(data), ctypes.byref(h)) != 0:
-        raise ValueError("OBJ parse failed: " + lib().rt_obj_last_error().decode(errors="replace"))
+    H = host_lib()
+    if H.rt_obj_parse(data, len(data), ctypes.byref(h)) != 0:
+        raise ValueError("OBJ parse failed: " + H.rt_obj_last_error().decode(errors="replace"))
     try:
-        n = [int(lib().rt_obj_size(h, k)) for k in range(5)]
+        n = [int(H.rt_obj_size(h, k)) for k in range(5)]
         vp, vn, vuv = (np.zeros(n[k], np.float32) for k in range(3))
         face = np.zeros(n[3], np.int32)
-        lib().rt_obj_copy(h, vp.ctypes.data, vn.ctypes.data, vuv.ctypes.data, face.ctypes.data)
+        H.rt_obj_copy(h, vp.ctypes.data, vn.ctypes.data, vuv.ctypes.data, face.ctypes.data)
     finally:
-        lib().rt_obj_free(h)
+        H.rt_obj_free(h)
     return vp, vn, vuv, face, n[4]
+
+
+def scene_check(V_p, V_n, faceData, materialData, bvh, layout: int = RT_BVH_SAH) -> dict:
+    """rt_scene_check (include/rt_scene.h): the validation and repacking rt_set_scene applies, on the
+    host alone (no GPU).  Raises NativeError with rt_set_scene's status for arrays it would refuse;
+    returns the packed layout's sizes and, when the FAST layouts are unavailable, why."""
+    vp, vn, face, mat, b = f32(V_p), f32(V_n), i32(faceData), f32(materialData), f32(bvh)
+    info = np.zeros(8, np.int64)
+    H = host_lib()
+    st = H.rt_scene_check(ptr(vp), vp.size, ptr(vn), vn.size, ptr(face), face.size, ptr(mat), mat.size,
+                          ptr(b), b.size, int(layout), info.ctypes.data)
+    msg = H.rt_scene_last_error().decode(errors="replace")
+    if st != 0:
+        raise NativeError(st, msg)
+    return dict(tris=int(info[0]), nodes=int(info[1]), depth=int(info[2]), wnodes=int(info[3]),
+                wdepth=int(info[4]), brute_records=int(info[5]), brute_boxes=int(info[6]), fast_ok=bool(info[7]),
+                note=msg)
 
 
 def tile_rows(npix: int, width: int, row0: int, row_step: int) -> int:

@@ -29,7 +29,7 @@ def build_export_array(faceData, V_p) -> np.ndarray:
         return np.zeros(0, dtype=np.float32)
     out = np.zeros(9 * (2 * T - 1), dtype=np.float32)
     nodes = ctypes.c_int64(0)
-    st = _native.lib().rt_bvh_build(face.ctypes.data, face.size, vp.ctypes.data, vp.size, out.ctypes.data,
+    st = _native.host_lib().rt_bvh_build(face.ctypes.data, face.size, vp.ctypes.data, vp.size, out.ctypes.data,
                                     ctypes.byref(nodes))
     if st == 3:
         raise DegenerateBVHError("a split left one side empty: the reference BVH.py would recurse forever "

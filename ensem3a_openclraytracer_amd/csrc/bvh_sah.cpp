@@ -13,9 +13,12 @@
 // Build: top-down; ranges of up to kSweepMax leaves use an exact sweep over
 // the centroids sorted along each axis, larger ranges 32 bins per axis.
 #include <algorithm>
+#include <atomic>
 #include <cstdint>
 #include <cstring>
+#include <limits>
 #include <numeric>
+#include <thread>
 #include <vector>
 
 #include "bvh_sah.h"
@@ -31,6 +34,7 @@ namespace {
 #endif
 constexpr int kSweepMax = RT_SAH_SWEEP_MAX;
 constexpr int kBins = RT_SAH_BINS;
+constexpr int kParMin = 4096;   // subtrees of at least this many leaves go to the thread pool
 
 struct Box {
     float lo[3], hi[3];
@@ -47,14 +51,23 @@ struct Box {
     }
 };
 
-struct Builder {
+// Bin of a centroid: the truncation (int)((c - cmin) * scale) clamped to [0, kBins), computed without
+// converting a non-finite or out-of-range double to int (caller-supplied boxes may hold NaN or inf)
+inline int bin_of(double c, double cmin, double scale) {
+    const double f = (c - cmin) * scale;
+    return f >= (double)(kBins - 1) ? kBins - 1 : f > 0.0 ? (int)f : 0;
+}
+
+// Centroid sort key: NaN ordered after everything, so the comparator stays a strict weak order
+inline double sort_key(double c) { return c == c ? c : std::numeric_limits<double>::infinity(); }
+
+// The leaves' boxes, centroids and the permutation every builder partitions in place (disjoint ranges).
+struct Shared {
     const std::vector<Box>& box;
     std::vector<double> cen;          // 3 per leaf
     std::vector<int32_t> idx;
-    SahTree& out;
-    std::vector<double> suffix;       // scratch for the sweep
 
-    Builder(const std::vector<Box>& b, SahTree& o) : box(b), out(o) {
+    explicit Shared(const std::vector<Box>& b) : box(b) {
         const size_t n = b.size();
         cen.resize(3 * n);
         for (size_t i = 0; i < n; ++i)
@@ -62,6 +75,23 @@ struct Builder {
         idx.resize(n);
         std::iota(idx.begin(), idx.end(), 0);
     }
+};
+
+// A split depends only on the leaves of its own range (their order in idx included), so subtrees over
+// disjoint ranges are built independently -- in parallel below a grain size -- and the tree is the one
+// the serial top-down build makes (node numbering aside, which nothing downstream reads: emit_bvh
+// renumbers breadth-first from the root).
+struct Builder {
+    const std::vector<Box>& box;
+    const std::vector<double>& cen;
+    std::vector<int32_t>& idx;
+    SahTree& out;
+    // scratch reused across calls: the build allocates nothing per node (allocator contention made the
+    // threaded build no faster than the serial one)
+    std::vector<double> suffix;       // the sweep's right-side costs
+    std::vector<int32_t> tmp, keep, part;
+
+    Builder(Shared& sh, SahTree& o) : box(sh.box), cen(sh.cen), idx(sh.idx), out(o) {}
 
     int32_t new_node() {
         out.L.push_back(-1);
@@ -92,12 +122,18 @@ struct Builder {
                 cmax[a] = std::max(cmax[a], cen[3 * idx[i] + a]);
             }
         if (n <= kSweepMax) {
-            std::vector<int32_t> tmp(idx.begin() + b, idx.begin() + e), keep;
+            tmp.assign(idx.begin() + b, idx.begin() + e);
             suffix.assign(n + 1, 0.0);
             for (int a = 0; a < 3; ++a) {
                 if (!(cmax[a] > cmin[a])) continue;
-                std::stable_sort(tmp.begin(), tmp.end(),
-                                 [&](int32_t x, int32_t y) { return cen[3 * x + a] < cen[3 * y + a]; });
+                // stable insertion sort by centroid (n <= kSweepMax): the order std::stable_sort gives
+                for (int i = 1; i < n; ++i) {
+                    const int32_t x = tmp[i];
+                    const double kx = sort_key(cen[3 * x + a]);
+                    int j = i;
+                    for (; j > 0 && kx < sort_key(cen[3 * tmp[j - 1] + a]); --j) tmp[j] = tmp[j - 1];
+                    tmp[j] = x;
+                }
                 Box acc;
                 acc.reset();
                 for (int i = n - 1; i >= 1; --i) {
@@ -127,8 +163,7 @@ struct Builder {
             int cnt[kBins] = {0};
             for (auto& x : bb) x.reset();
             for (int i = b; i < e; ++i) {
-                int k = (int)((cen[3 * idx[i] + a] - cmin[a]) * scale);
-                k = std::min(std::max(k, 0), kBins - 1);
+                const int k = bin_of(cen[3 * idx[i] + a], cmin[a], scale);
                 cnt[k]++;
                 bb[k].grow(box[idx[i]]);
             }
@@ -153,23 +188,32 @@ struct Builder {
         }
         if (best_axis < 0) return b + n / 2;
         const double scale = kBins / (cmax[best_axis] - cmin[best_axis]);
-        auto mid = std::stable_partition(idx.begin() + b, idx.begin() + e, [&](int32_t x) {
-            int k = (int)((cen[3 * x + best_axis] - cmin[best_axis]) * scale);
-            k = std::min(std::max(k, 0), kBins - 1);
-            return k < best_bin;
-        });
-        return (int)(mid - idx.begin());
+        // stable partition (the order std::stable_partition gives) through the reused scratch
+        part.clear();
+        int m = b;
+        for (int i = b; i < e; ++i) {
+            const int32_t x = idx[i];
+            if (bin_of(cen[3 * x + best_axis], cmin[best_axis], scale) < best_bin) idx[m++] = x;
+            else part.push_back(x);
+        }
+        std::copy(part.begin(), part.end(), idx.begin() + m);
+        return m;
     }
 
-    void build() {
-        const int n = (int)idx.size();
-        if (n == 0) return;
-        struct Item { int b, e; int32_t node; };
+    struct Item { int b, e; int32_t node; };
+
+    // Top-down from the range [b, e) at node `root`; ranges of at most `grain` leaves (other than the
+    // root's own) are not built but returned in `deferred`.
+    void build(int b0, int e0, int32_t root, int grain, std::vector<Item>* deferred) {
         std::vector<Item> work;
-        work.push_back({0, n, new_node()});
+        work.push_back({b0, e0, root});
         while (!work.empty()) {
             const Item it = work.back();
             work.pop_back();
+            if (deferred && it.node != root && it.e - it.b <= grain) {
+                deferred->push_back(it);
+                continue;
+            }
             set_box(it.node, it.b, it.e);
             if (it.e - it.b == 1) {
                 out.leaf[it.node] = idx[it.b];
@@ -202,8 +246,49 @@ void sah_build(const float* leaf_boxes, const int32_t* leaf_ids, int64_t n, SahT
     out.R.reserve(2 * n);
     out.leaf.reserve(2 * n);
     out.box.reserve(12 * n);
-    Builder bld(boxes, out);
-    bld.build();
+    if (n == 0) return;
+    Shared sh(boxes);
+    Builder top(sh, out);
+    const int32_t root = top.new_node();
+    const unsigned hw = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    if (hw == 1 || n < 4 * kParMin) {
+        top.build(0, (int)n, root, 0, nullptr);
+    } else {
+        // the top of the tree serially, down to ranges of `grain` leaves; those subtrees on hw threads
+        const int grain = std::max<int>(kParMin, (int)(n / (8 * (int64_t)hw)));
+        std::vector<Builder::Item> tasks;
+        top.build(0, (int)n, root, grain, &tasks);
+        std::vector<SahTree> sub(tasks.size());
+        std::atomic<size_t> next{0};
+        auto worker = [&]() {
+            for (size_t k; (k = next.fetch_add(1)) < tasks.size();) {
+                Builder bb(sh, sub[k]);
+                const int32_t r = bb.new_node();
+                bb.build(tasks[k].b, tasks[k].e, r, 0, nullptr);
+            }
+        };
+        std::vector<std::thread> pool;
+        for (unsigned t = 1; t < hw; ++t) pool.emplace_back(worker);
+        worker();
+        for (auto& t : pool) t.join();
+        // stitch: subtree k's node 0 becomes the deferred node, its other nodes are appended
+        for (size_t k = 0; k < tasks.size(); ++k) {
+            const SahTree& st = sub[k];
+            const int32_t base = (int32_t)out.L.size() - 1;   // local node j >= 1 -> base + j
+            auto map = [&](int32_t j) { return j < 0 ? j : j == 0 ? tasks[k].node : base + j; };
+            const int32_t dn = tasks[k].node;
+            out.L[dn] = map(st.L[0]);
+            out.R[dn] = map(st.R[0]);
+            out.leaf[dn] = st.leaf[0];
+            for (int c = 0; c < 6; ++c) out.box[6 * (size_t)dn + c] = st.box[c];
+            for (size_t j = 1; j < st.L.size(); ++j) {
+                out.L.push_back(map(st.L[j]));
+                out.R.push_back(map(st.R[j]));
+                out.leaf.push_back(st.leaf[j]);
+                out.box.insert(out.box.end(), st.box.begin() + 6 * j, st.box.begin() + 6 * j + 6);
+            }
+        }
+    }
     for (auto& t : out.leaf)
         if (t >= 0) t = leaf_ids[t];
 }

@@ -13,6 +13,7 @@
 //   * any other line starting with 'u' increments the material counter.
 // A face field the reference's int() would reject makes the parse fail.
 #include <charconv>
+#include <climits>
 #include <cmath>
 #include <cstdint>
 #include <cstdlib>
@@ -62,11 +63,13 @@ bool parse_int(const char* b, const char* e, long long* out) {
     if (*b == '+' || *b == '-') neg = *b++ == '-';
     if (b == e) return false;
     long long v = 0;
+    bool big = false;   // beyond 2^32: no int32 faceData entry can hold it
     for (const char* q = b; q < e; ++q) {
         if (*q < '0' || *q > '9') return false;
-        v = v * 10 + (*q - '0');
+        if (!big) v = v * 10 + (*q - '0');
+        big = big || v > (1ll << 32);
     }
-    *out = neg ? -v : v;
+    *out = big ? (neg ? -(1ll << 40) : (1ll << 40)) : (neg ? -v : v);
     return true;
 }
 
@@ -172,6 +175,12 @@ int rt_obj_parse(const char* text, int64_t len, rt_obj** out) {
                     if (!parse_int(s, sl ? sl : fe, &v)) {
                         delete o;
                         return fail("line " + std::to_string(lineno) + ": bad face index");
+                    }
+                    // the reference stores faceData as int32 (FileManager.py:276-282): an index it cannot hold
+                    // is refused here rather than wrapped
+                    if (v - 1 < INT32_MIN || v - 1 > INT32_MAX) {
+                        delete o;
+                        return fail("line " + std::to_string(lineno) + ": face index out of the int32 range");
                     }
                     row[w++] = (int32_t)(v - 1);
                 }

@@ -464,16 +464,17 @@ hipError_t launch_spec(const DevScene& sc, const FrameParams& fp, int block, flo
     {
         // blocks per CU of each (instantiation, block, LDS), queried once: an automatic pass 2 launches all
         // three trail kernels of which at most one renders, and the host query costs more than their launches
-        struct Occ { const void* fn; int block; size_t lds; int per_cu; };
+        // (keyed by device too: a context may hold devices of different kinds)
+        struct Occ { int dev; const void* fn; int block; size_t lds; int per_cu; };
         static std::mutex mu;
         static std::vector<Occ> seen;
         std::lock_guard<std::mutex> g(mu);
         for (const Occ& o : seen)
-            if (o.fn == fn && o.block == block && o.lds == lds) per_cu = o.per_cu;
+            if (o.dev == dev && o.fn == fn && o.block == block && o.lds == lds) per_cu = o.per_cu;
         if (per_cu == 0) {
             e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, block, lds);
             if (e != hipSuccess) return e;
-            seen.push_back({fn, block, lds, per_cu});
+            seen.push_back({dev, fn, block, lds, per_cu});
         }
     }
     const int cap_cu = fp.max_waves > 0 ? std::max(1, fp.max_waves * 4 * 64 / block) : INT_MAX;

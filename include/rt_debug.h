@@ -46,6 +46,13 @@ int rt_debug_wave_counts(rt_ctx* ctx, const float cam[10], const float env[5], i
  * the 4-wide walk dequantises origin-folded, in millionths (0: never), out[7] = 0. */
 int rt_debug_scene_info(rt_ctx* ctx, int64_t out[8]);
 
+/* Host wall times (ms) of the context's last calls, the parts of SURVEY.md 8(d)'s cold t_render
+ * (KernelLauncher.py:33-87 pays all of them on every launch_Raytracing): [0] rt_set_scene's validation
+ * and repacking (SAH / 4-wide layouts), [1] its uploads and the per-triangle frame kernel, [2]
+ * rt_set_env (IBL upload + texel-sum kernel), [3] the last blocking rt_render / rt_render_rgb8
+ * (render + read-back). */
+int rt_debug_timings(rt_ctx* ctx, double out[4]);
+
 /* Host-only (no device): the per-axis quantisation of the 4-wide layout (rt_api.hip emit_wide).
  * For up to n = 4 child intervals [lo[c], hi[c]] against the lower corner p, returns the biased
  * exponent byte e (scale 2^(e-127)) and byte bounds with p + qlo[c] * 2^(e-127) <= lo[c] and

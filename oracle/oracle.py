@@ -39,9 +39,12 @@ def build() -> str:
 def lib():
     global _lib
     if _lib is None:
-        if not os.path.exists(_LIB_PATH):
-            build()
-        _lib = ctypes.CDLL(_LIB_PATH)
+        path = os.environ.get("ENSEM3A_ORACLE_LIB")   # the sanitizer build (tools/sanitize.sh)
+        if not path:
+            path = _LIB_PATH
+            if not os.path.exists(path):
+                build()
+        _lib = ctypes.CDLL(path)
         _lib.oracle_render.restype = ctypes.c_int
         _lib.oracle_render.argtypes = [ctypes.POINTER(_Scene), ctypes.c_void_p, ctypes.c_void_p,
                                        ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,

@@ -1232,6 +1232,31 @@ def test_speculative_trails_render_identically(kl, case):
         kl.native.set_option("spec", 3)
 
 
+def test_speculative_trails_past_the_log_cap(kl):
+    """A trail's log holds at most kSpecCapMax (256) records; with spp - pilot > 256 a trail parks at the
+    cap and the chain goes on in a trail further ahead or in trail 0 (rt_api.hip setup of spec_cap).  At
+    400 samples after a 2-sample pilot that path runs on every pixel: 2, 4 and 8 trails give the one-lane
+    frame, and the oracle's, bit for bit (r05 ADVICE)."""
+    sc, cam, env, npix, _, mb, ibl = W.PARITY_CASES["serre_96x54_s4"].inputs()
+    spp = 402
+    want = _oracle(sc, cam, env, npix, spp, mb, ibl)
+    kl.native.set_option("brute_max", 0)
+    kl.native.set_option("bvh_width", 2)
+    kl.native.set_option("pilot", 2)
+    try:
+        frames = {}
+        for trails in (0, 2, 4, 8):
+            kl.native.set_option("spec", trails)
+            frames[trails] = _launch(kl, sc, cam, env, npix, spp, mb, ibl, "fast")
+    finally:
+        kl.native.set_option("spec", -1)
+        kl.native.set_option("pilot", -1)
+        kl.native.set_option("bvh_width", 0)
+        kl.native.set_option("brute_max", 64)
+    for key, f in frames.items():
+        np.testing.assert_array_equal(f, want, err_msg=f"spec {key}")
+
+
 @pytest.mark.parametrize("config,row0,step", [("C3", 3, 8), ("C4", 5, 8), ("C3", 2, 5), ("C4", 0, 3)])
 def test_speculative_trails_row_tiles(kl, config, row0, step):
     """A 1/8 row tile of the full-size C3 / C4 frame (the multi-GPU regime) at 64 spp with the automatic
@@ -1257,21 +1282,28 @@ def test_speculative_trails_row_tiles(kl, config, row0, step):
         np.testing.assert_array_equal(f, frames[0])
 
 
-@pytest.mark.parametrize("case", ["monkey_c3_64_s4", "serre_96x54_s4", "proto_64_s4", "grid"])
+@pytest.mark.parametrize("case", ["monkey_c3_64_s4", "serre_96x54_s4", "proto_64_s4", "grid", "monkey_partial_row"])
 def test_sample_slices_render_identically(kl, case):
     """slices K: a pixel's samples are K jobs handed out slice-major; the job of slice k continues the pixel
     from the state the job of slice k - 1 published (on any lane, any XCD).  Every pixel's samples run in
     order, so the frame is the one-pass frame and the oracle's, bit for bit, on both tree layouts (the grid
-    case: the 4-wide walk, slices on by default), whole frames and row tiles, both hand-out orders."""
+    case: the 4-wide walk, slices on by default), whole frames and row tiles, both hand-out orders.
+    monkey_partial_row: imgDim = 64 * 63 + 17, so padding pixels of the partial last row sit inside every
+    slice pass; a lane that meets one must go on to the next job, not retire (r05 ADVICE)."""
     import torch
     from ensem3a_openclraytracer_amd import distributed as D
     if case == "grid":
         sc, cam, env, npix, spp, mb, ibl = W.CONFIGS["C5"].with_size(48, 27, 16).inputs()
+    elif case == "monkey_partial_row":
+        sc, cam, env, npix, _, mb, ibl = W.PARITY_CASES["monkey_c3_64_s4"].inputs()
+        npix, spp = 64 * 63 + 17, 16
     else:
         sc, cam, env, npix, _, mb, ibl = W.PARITY_CASES[case].inputs()
         spp = 16
-    want = _oracle(sc, cam, env, npix, spp, mb, ibl)
+    want = _oracle(sc, cam, env, npix, spp, mb, ibl)[: 3 * npix]   # the oracle renders whole rows
     w = int(cam[6])
+    rows_full = -(-npix // w)
+    want_rows = np.concatenate([want, np.zeros(3 * (rows_full * w - npix), np.float32)]).reshape(-1, 3 * w)
     kl.native.set_option("pilot", 0)   # slices are for one-pass launches (the BVH2 walk's small frames take a pilot)
     try:
         for width in (2, 4):
@@ -1282,11 +1314,14 @@ def test_sample_slices_render_identically(kl, case):
                     kl.native.set_option("handout", h)
                     np.testing.assert_array_equal(_launch(kl, sc, cam, env, npix, spp, mb, ibl, "fast"), want,
                                                   err_msg=f"width {width} slices {k} handout {h}")
-                t = torch.zeros(3 * w * D.tile_rows(npix, w, 1, 3), dtype=torch.float32, device="cuda")
-                kl.native.render_device(cam, env, npix, spp, mb, 1, 3, t.data_ptr())
+                r0 = (rows_full - 1) % 3 if npix % w else 1   # a partial last row: the tile that holds it
+                t = torch.zeros(3 * w * D.tile_rows(npix, w, r0, 3), dtype=torch.float32, device="cuda")
+                kl.native.render_device(cam, env, npix, spp, mb, r0, 3, t.data_ptr())
                 torch.cuda.synchronize()
-                np.testing.assert_array_equal(t.cpu().numpy(), want.reshape(-1, 3 * w)[1::3].ravel(),
-                                              err_msg=f"width {width} slices {k} tile 1::3")
+                got_t = t.cpu().numpy().reshape(-1, 3 * w)
+                if npix % w:
+                    got_t[-1, 3 * (npix % w):] = 0   # the tile's padding past the frame is not compared
+                np.testing.assert_array_equal(got_t, want_rows[r0::3], err_msg=f"width {width} slices {k} tile {r0}::3")
     finally:
         kl.native.set_option("slices", -1)
         kl.native.set_option("handout", -1)
