@@ -261,7 +261,6 @@ int check_frame(rt_ctx* ctx, const float* cam, const float* env, int64_t npix, i
     fp->slices = 0;
     fp->slice_state = nullptr;
     fp->slice_ready = nullptr;
-    fp->walk_team_dev = nullptr;
     fp->pilot_cost = nullptr;
     fp->pilot_order = nullptr;
     fp->team = ctx->team;

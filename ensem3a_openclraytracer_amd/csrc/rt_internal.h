@@ -81,7 +81,6 @@ struct FrameParams {
     int32_t resume_min;  // FAST tree walk: resumable traversal, shade once this many lanes are free (0 = off)
     int32_t team;        // brute-force path: lanes per pixel (1, 2, 4, 8; 0 = chosen at launch from the tile size)
     int32_t walk_team;   // FAST tree walk (BVH2 item steps): lanes per pixel walking each ray together (1, 2, 4, 8; 0 = auto)
-    const int32_t* walk_team_dev;   // pass 2 of a pilot launch with walk_team auto: the team size, chosen on the device
     int32_t max_waves;   // persistent grid: at most this many waves per SIMD (0 = as many as stay resident)
     int32_t handout;     // pixel hand-out: 0 = chunks interleaved over the XCD groups, 1 = a contiguous block per group
     int32_t step;        // FAST tree walk: 1 = one item per traversal step, 2 = descend-until-leaf rounds, 0 = auto
@@ -148,7 +147,7 @@ hipError_t launch_rgb8(const float* d_in, uint8_t* d_out, int64_t n, bool gamma,
 // Sample-parallel speculation (rt_spec.hip): pass 2 of a pilot launch of the BVH2 walk with fp.spec
 // trails per pixel; spec_log_bytes = the size of fp.spec_log it needs on a device of `cus` CUs (one log
 // per resident lane, launch_spec keeps the grid within them); at most kSpecTrails trails per pixel;
-// the device pick of pass 2 encodes "T trails" as kSpecPick + T in FrameParams::walk_team_dev
+// the device pick of pass 2 (pilot_team_pick_kernel, read back by launch_render) encodes "T trails" as kSpecPick + T
 constexpr int kSpecTrails = 8;
 constexpr int kSpecPick = 10;
 constexpr int kSpecCapMax = 256;   // records per trail log at most (FrameParams::spec_cap)

@@ -171,8 +171,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) r
                         phase = s >= spp ? FETCH : PREP;   // finished in pass 1: already written
                     }
                 } else {
-                    // past the tile, or (pass 2, pixels in cost order) a padding pixel past the frame
-                    phase = (F.pass == 2 && q < nloc) ? FETCH : DONE;
+                    // past the tile, or a padding pixel of a partial last row (its hand-out group, or pass 2's
+                    // cost order, may still hold real pixels): the lane retires once the queue is dry
+                    phase = q < nloc ? FETCH : DONE;
                 }
             }
         }
@@ -368,9 +369,6 @@ constexpr size_t kStepMaxBytes = 16u << 20;
 // (kWideWaves: rt_internal.h)
 
 // TS > 1: teams of TS lanes per pixel walk each ray together (team_step; BVH2 item steps only).
-// F.walk_team_dev (pass 2 of a pilot launch): the team size was chosen on the device from the pixels
-// pass 1 left unfinished (pilot_team_pick_kernel); the instantiations of the other sizes, launched
-// beside this one, return at once.
 // WIDE: 0 = the BVH2 walk, 1 = the 4-wide walk, 2 = the 4-wide walk with origin-folded dequantisation
 // (wide_node DQ; launch_fast picks it when the camera lies within DevScene::wdq_omax)
 template <bool COUNT, bool LOG, bool SMEM, bool OVF, bool STEP, int WIDE, int TS = 1>
@@ -378,8 +376,6 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WIDE ?
                                                       unsigned long long* __restrict__ counts,
                                                       unsigned int* __restrict__ work_counter,
                                                       const LaunchConst* __restrict__ lconst) {
-    // pass 2 with the team size chosen on the device: only the instantiation of that size renders
-    if (F.walk_team_dev && __builtin_amdgcn_readfirstlane(*F.walk_team_dev) != TS) return;
     extern __shared__ int lds_stack[];
     const int B = blockDim.x;
     // two-pass launches are BVH2-only (the 4-wide walk's pilot measured slower, rt_api.hip setup_pilot):
@@ -903,12 +899,11 @@ hipError_t launch_t(const DevScene& sc, const FrameParams& fp, int block, float*
     // blocks per CU for at most max_waves waves per SIMD (4 SIMDs per CU)
     const int cap_cu = fp.max_waves > 0 ? std::max(1, fp.max_waves * 4 * 64 / block) : INT_MAX;
     const int64_t resident = (int64_t)std::max(1, cus) * std::max(1, std::min(per_cu, cap_cu));
-    // team walk (render_resume_kernel TEAM): BVH2 item steps only.  walk_team_dev: the team size is
-    // chosen on the device (pass 2 of a pilot launch); otherwise walk_team, 0 = auto (auto_walk_team)
+    // team walk (render_resume_kernel TEAM): BVH2 item steps only; walk_team, 0 = auto (auto_walk_team;
+    // pass 2 of a pilot launch: the size pilot_team_pick_kernel chose, launch_render)
     constexpr bool kTeamable = RESUME && STEP && !WIDE && !LOG;
     int wteam = 1;
-    const bool dev_team = kTeamable && fp.walk_team_dev != nullptr;
-    if (kTeamable && !dev_team) {
+    if (kTeamable) {
         wteam = fp.walk_team;
         if (wteam == 0) wteam = auto_walk_team(fp.nloc, resident * block);
         if (wteam != 2 && wteam != 4 && wteam != 8) wteam = 1;
@@ -929,7 +924,6 @@ hipError_t launch_t(const DevScene& sc, const FrameParams& fp, int block, float*
         }
     }
     f.walk_team = wteam;
-    if (!dev_team) f.walk_team_dev = nullptr;
     const int64_t need = (fp.nloc * f.team * wteam + block - 1) / block;
     int64_t grid = std::min(need, resident);
     // the team instantiations (TS = 2, 4, 8) and their own occupancy
@@ -946,7 +940,7 @@ hipError_t launch_t(const DevScene& sc, const FrameParams& fp, int block, float*
                       (int64_t)std::max(1, cus) * std::max(1, std::min(per_cu_w, cap_cu)));
         return er;
     };
-    if (kTeamable && wteam > 1 && !dev_team) {
+    if (kTeamable && wteam > 1) {
         e = team_grid(wteam, &grid);
         if (e != hipSuccess) return e;
     }
@@ -965,22 +959,7 @@ hipError_t launch_t(const DevScene& sc, const FrameParams& fp, int block, float*
                   "work block layout");
     LaunchConst* lc = reinterpret_cast<LaunchConst*>(reinterpret_cast<char*>(d_work) + kConstOffset);
     hipLaunchKernelGGL(make_const_kernel, dim3(1), dim3(64), 0, stream, f, lc);
-    if (kTeamable && dev_team) {
-        // the device picks 1, 2 or 4 lanes (pilot_team_pick_kernel): all three are launched in order, and the
-        // two whose size was not picked return at once
-        int64_t g2 = 0, g4 = 0;
-        e = team_grid(2, &g2);
-        if (e == hipSuccess) e = team_grid(4, &g4);
-        if (e != hipSuccess) return e;
-        hipLaunchKernelGGL((render_resume_kernel<COUNT, LOG, SMEM, OVF, STEP, WIDE, 1>), dim3((unsigned)grid),
-                           dim3(block), lds, stream, sc, f, d_out, d_counts, d_work, (const LaunchConst*)lc);
-        hipLaunchKernelGGL((render_resume_kernel<COUNT, LOG, SMEM, OVF, STEP, WIDE, kTeamable ? 2 : 1>),
-                           dim3((unsigned)g2), dim3(block), lds, stream, sc, f, d_out, d_counts, d_work,
-                           (const LaunchConst*)lc);
-        hipLaunchKernelGGL((render_resume_kernel<COUNT, LOG, SMEM, OVF, STEP, WIDE, kTeamable ? 4 : 1>),
-                           dim3((unsigned)g4), dim3(block), lds, stream, sc, f, d_out, d_counts, d_work,
-                           (const LaunchConst*)lc);
-    } else if (kTeamable && wteam == 2)
+    if (kTeamable && wteam == 2)
         hipLaunchKernelGGL((render_resume_kernel<COUNT, LOG, SMEM, OVF, STEP, WIDE, kTeamable ? 2 : 1>),
                            dim3((unsigned)grid), dim3(block), lds, stream, sc, f, d_out, d_counts, d_work,
                            (const LaunchConst*)lc);
@@ -1311,18 +1290,17 @@ hipError_t launch_render(const DevScene& sc, const FrameParams& fp, int traversa
         // resident lanes of the one-lane BVH2 walk: 4 waves per SIMD
         hipLaunchKernelGGL(pilot_team_pick_kernel, dim3(1), dim3(64), 0, stream, left,
                            (int64_t)std::max(cus, 1) * kWalkLanesPerCu, spec_ok ? 1 : 0, ts);
-        b.walk_team_dev = ts;
-        if (spec_ok) {
-            // the one-lane walk (the team instantiations return at once: a trail pick is no team size), then
-            // the 2- and 4-trail kernels, of which at most the one picked renders
-            e = launch_render_pass(sc, b, traversal, block, d_out, nullptr, d_work, stream);
-            for (int trails = 2; e == hipSuccess && trails <= kSpecTrails; trails *= 2) {
-                FrameParams t = b;
-                t.spec = trails;
-                e = launch_spec(sc, t, block, d_out, d_work, stream);
-            }
-            return e;
+        // the pick is read back (pass 1 has to finish before pass 2 anyway) and exactly the kernel it names
+        // is launched: 1, 2 or 4 lanes per pixel, or kSpecPick + T trails
+        int pick = 1;
+        e = hipMemcpyAsync(&pick, ts, sizeof(int), hipMemcpyDeviceToHost, stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(stream);
+        if (e != hipSuccess) return e;
+        if (spec_ok && pick > kSpecPick) {
+            b.spec = pick - kSpecPick;
+            return launch_spec(sc, b, block, d_out, d_work, stream);
         }
+        b.walk_team = pick;
     }
     return launch_render_pass(sc, b, traversal, block, d_out, nullptr, d_work, stream);
 }

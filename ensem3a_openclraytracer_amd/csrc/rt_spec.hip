@@ -49,8 +49,6 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4)))
 spec_kernel(DevScene S, FrameParams F, float* __restrict__ out, unsigned int* __restrict__ work_counter,
             const LaunchConst* __restrict__ lconst) {
     static_assert(TR == 2 || TR == 4 || TR == 8, "trails per pixel");
-    // trails chosen on the device (pilot_team_pick_kernel): only the instantiation picked renders
-    if (F.walk_team_dev && __builtin_amdgcn_readfirstlane(*F.walk_team_dev) != kSpecPick + TR) return;
     extern __shared__ int lds_stack[];
     Cnt c{};
     const LaunchConst& C = *lconst;
@@ -462,9 +460,8 @@ hipError_t launch_spec(const DevScene& sc, const FrameParams& fp, int block, flo
     if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     if (e != hipSuccess) return e;
     {
-        // blocks per CU of each (instantiation, block, LDS), queried once: an automatic pass 2 launches all
-        // three trail kernels of which at most one renders, and the host query costs more than their launches
-        // (keyed by device too: a context may hold devices of different kinds)
+        // blocks per CU of each (instantiation, block, LDS), queried once per device (a context may hold
+        // devices of different kinds): the host query costs more than the launch
         struct Occ { int dev; const void* fn; int block; size_t lds; int per_cu; };
         static std::mutex mu;
         static std::vector<Occ> seen;

@@ -73,36 +73,19 @@ int rt_set_scene(rt_ctx* ctx, const float* vp, int64_t nvp, const float* vn, int
  * cl.Image of KernelLauncher.py:71-72). */
 int rt_set_env(rt_ctx* ctx, const uint8_t* rgba, int w, int h);
 
-/* Integer options: "traversal" (rt_traversal), "bvh" (rt_bvh_layout),
- * "brute_max" (FAST on scenes of at most this many triangles tests every
- * triangle in lock-step instead of walking the tree -- same hits; default 64,
- * 0 = always walk the tree),
- * "resume_min" (FAST tree walk: 0 = each wave traces until all its rays are
- * done; 1..64 = rays keep their traversal state across render-loop
- * iterations and the wave shades as soon as this many lanes are free -- same
- * hits), "step" (resumable tree walk: 1 = one node or leaf per traversal
- * step, 2 = descend to a leaf per step, 0 = auto by node-array size -- same
- * hits), "team" (brute force: lanes per pixel 1/2/4/8, 0 = auto by tile
- * size), "walk_team" (BVH2 tree walk: 1/2/4/8 lanes walk each ray of a pixel
- * together, 0 = auto: 4 on tiles of at most one pixel per resident lane and
- * on the second pass of a pilot launch from the pixels its first pass left --
- * same hits), "spec" (second pass of a pilot launch of the BVH2 walk: 2/4/8
- * speculative trails per pixel from guessed RNG offsets, stitched in chain
- * order, 0 = off, -1 = auto: chosen on the device on small tiles -- same
- * frame), "slices" (one-pass tree-walk launches: each pixel's samples as K
- * jobs handed out slice-major, 0 = off, -1 = auto: 8 on the 4-wide walk --
- * same frame), "handout" (1 = a contiguous pixel block per XCD group, 0 =
- * interleaved chunks, -1 = auto: 1 on the 4-wide walk), "wdq" (4-wide walk:
- * 1 = child boxes dequantised origin-folded where the layout's quantisation gap
- * covers the frame's camera, 0 = always the (p + q s) - o form -- same frame),
- * "waves" (persistent
- * grid: at most this many waves per SIMD, 0 = occupancy limit), "block"
- * (threads per block: 64, 128 or 256), and the tuning switches documented in
- * DESIGN.md 4.2 ("sun_skip", "sun_any", "fixed_point", "sun_cache", "pilot",
- * "pilot_chunk", "pilot_levels", "stack_lds", "ref_stack",
- * "bvh_width"): every option renders the same frame except "ref_stack" (REF's
- * stack slots; 20 = the reference's, more = no silent drops).
- * "bvh" and "brute_max" may be changed after rt_set_scene. */
+/* Integer options of the drop-in contract:
+ *   "traversal"  rt_traversal (FAST default; REF = the reference's own DFS, stack.cl's 20 slots);
+ *   "bvh"        rt_bvh_layout the FAST walk uses (SAH default) -- same hits;
+ *   "bvh_width"  FAST tree walk: 2 = BVH2 nodes, 4 = the 4-wide quantised layout, 0 = auto (4-wide when
+ *                the BVH2 node array exceeds 16 MB) -- same frame;
+ *   "brute_max"  FAST on scenes of at most this many triangles tests every leaf box in lock-step instead
+ *                of walking a tree (default 64, 0 = always walk) -- same hits;
+ *   "ref_stack"  REF's stack slots (20 = the reference's; more = no silent drops: the only option that
+ *                changes a frame);
+ *   "block"      threads per block: 64, 128 or 256.
+ * "bvh" and "brute_max" may be changed after rt_set_scene.  Every other key rt_set_option accepts is a
+ * scheduling / equivalence knob listed in rt_debug.h: each renders the same frame, and the automatic
+ * values are the measured defaults. */
 int rt_set_option(rt_ctx* ctx, const char* key, int64_t value);
 
 /* Render one frame, blocking, into caller-owned host memory out_rgb[3*npix]

@@ -7,6 +7,23 @@
 #include <stdint.h>
 #include "rt_api.h"
 
+/* Scheduling and equivalence knobs of rt_set_option (rt_api.h lists the contract's options).  Each
+ * renders the same frame as its automatic value (the GPU tests check that bit for bit); the automatic
+ * values are the measured defaults.  -1 / 0 = auto where noted.
+ *   "resume_min"   resumable tree walk: shade once this many of 64 lanes are free (-1 auto 36 / 48)
+ *   "step"         tree-walk traversal loop: 1 one item per step, 2 descend-until-leaf rounds (0 auto)
+ *   "team"         brute force: lanes per pixel 1/2/4/8 (0 auto by tile size)
+ *   "walk_team"    BVH2 walk: lanes walking each ray of a pixel together 1/2/4/8 (0 auto)
+ *   "spec"         pass 2 of a pilot launch: speculative trails per pixel 2/4/8 (0 off, -1 auto)
+ *   "slices"       one-pass tree-walk launches: sample slices per pixel 2..16 (0 off, -1 auto)
+ *   "pilot"        two-pass launches: pilot samples per pixel (0 one pass, -1 auto);
+ *   "pilot_chunk", "pilot_levels"  the pass-2 order's chunk of pixels and cost bins (0 auto)
+ *   "handout"      pixel hand-out: 1 a contiguous block per XCD group, 0 interleaved chunks (-1 auto)
+ *   "wdq"          4-wide walk: origin-folded dequantisation where the builder's gap covers the camera (1)
+ *   "waves"        persistent grid: at most this many waves per SIMD (0 = occupancy limit)
+ *   "stack_lds"    FAST stack entries per lane kept in LDS, deeper ones in HBM (0 auto)
+ *   "sun_skip", "sun_any", "fixed_point", "sun_cache"  exact shortcuts of the shading loop (1 = on) */
+
 #ifdef __cplusplus
 extern "C" {
 #endif

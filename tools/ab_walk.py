@@ -18,22 +18,28 @@ if len(sys.argv) > 2 and sys.argv[1] == "--one":
         ctx.set_scene(sc.V_p, sc.V_n, sc.V_uv, sc.faceData, sc.materialData, sc.BVH.exportArray)
         ctx.set_env(ibl)
         info = ctx.scene_info()
-        out = torch.empty(3 * npix, dtype=torch.float32, device="cuda")
-        ctx.render_device(cam, env, npix, 4, mb, 0, 1, out.data_ptr())
+        # AB_TILE=N: rank 0's tile of an N-GPU run (rows 0::N) instead of the whole frame; AB_REPS frames timed
+        step = int(os.environ.get("AB_TILE", "1"))
+        reps = int(os.environ.get("AB_REPS", "2"))
+        width = int(cam[6])
+        rows = (npix + width - 1) // width
+        out = torch.empty(3 * width * ((rows + step - 1) // step), dtype=torch.float32, device="cuda")
+        ctx.render_device(cam, env, npix, 4, mb, 0, step, out.data_ptr())
         torch.cuda.synchronize()
         small = out.cpu().numpy().copy()
-        np.save(f"/tmp/ab_{cfg}_{name}.npy", small)
-        ref = f"/tmp/ab_{cfg}_base.npy"
+        np.save(f"/tmp/ab_{cfg}_{step}_{name}.npy", small)
+        ref = f"/tmp/ab_{cfg}_{step}_base.npy"
         same = bool(np.array_equal(np.load(ref), small)) if os.path.exists(ref) else None
-        ctx.render_device(cam, env, npix, spp, mb, 0, 1, out.data_ptr())
+        ctx.render_device(cam, env, npix, spp, mb, 0, step, out.data_ptr())
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        for _ in range(2):
-            ctx.render_device(cam, env, npix, spp, mb, 0, 1, out.data_ptr())
+        for _ in range(reps):
+            ctx.render_device(cam, env, npix, spp, mb, 0, step, out.data_ptr())
         torch.cuda.synchronize()
-        dt = (time.perf_counter() - t0) / 2
-        print(json.dumps({"variant": name, "block": block, "cfg": cfg, "Msamples/s": round(npix * spp / dt / 1e6, 1),
-                          "ms": round(dt * 1e3, 2), "identical_4spp": same, "info": info}), flush=True)
+        dt = (time.perf_counter() - t0) / reps
+        print(json.dumps({"variant": name, "block": block, "cfg": cfg, "tile": step,
+                          "Msamples/s": round(npix * spp / step / dt / 1e6, 1),
+                          "ms": round(dt * 1e3, 3), "identical_4spp": same, "info": info}), flush=True)
         ctx.close()
 else:
     for spec in sys.argv[1].split(","):

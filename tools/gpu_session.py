@@ -15,12 +15,14 @@ STEP forms (values after '=' separated by ':'):
   benchfull                     the default bench.py run (what the driver records)
   smoke                         __graft_entry__.smoke()
   ab=CFGS:SPECS                 tools/ab_walk.py SPECS with AB_CFGS=CFGS (SPECS = name[@k=v+k=v]:block,...)
+  abt=TILE:REPS:CFGS:SPECS      the same on rank 0's tile of a TILE-GPU run (rows 0::TILE), REPS frames timed
   tiles=CFG:NS[:SETS]           tools/occupancy_probe.py CFG NS "SETS" (SETS: k=v,k=v;k=v)
   kt=CFG[:OPTS[:STEPS]]         rocprofv3 --kernel-trace --stats of bench.py (STEPS steps, default 1, after 1
                                 warmup) -> gpurun_out/TAG_kt_CFG
   pmc=CFG:GROUP[:OPTS[:STEPS]]  one rocprofv3 --pmc pass (GROUP: fetch, write, req, sq, hit, ta, stall) of bench.py
   py=SCRIPT[:ARGS]              python3 -u SCRIPT ARGS (ARGS split on '+')
   ktpy=NAME:SCRIPT[:ARGS]       rocprofv3 --kernel-trace --stats of a py step -> gpurun_out/TAG_kt_NAME
+  pmcpy=NAME:GROUP:SCRIPT[:ARGS] one rocprofv3 --pmc pass of a py step -> gpurun_out/TAG_pmc_NAME_GROUP
 Limits: LIMIT_<KIND> env overrides the default seconds of a step kind.
 """
 import os
@@ -31,8 +33,8 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 OUT = os.path.join(ROOT, "gpurun_out")
 PY = sys.executable or "python3"
-LIMITS = {"clock": 30, "pytest": 900, "bench": 300, "benchfull": 600, "smoke": 180, "ab": 600, "tiles": 400, "kt": 300,
-          "pmc": 240, "py": 600, "ktpy": 400}
+LIMITS = {"clock": 30, "pytest": 900, "bench": 300, "benchfull": 600, "smoke": 180, "ab": 600, "abt": 600, "tiles": 400, "kt": 300,
+          "pmc": 240, "py": 600, "ktpy": 400, "pmcpy": 240}
 PMC = {
     "fetch": "FETCH_SIZE",
     "write": "WRITE_SIZE",
@@ -77,6 +79,9 @@ def command(kind, val, tag, n):
     if kind == "ab":
         env["AB_CFGS"] = p[0]
         return [PY, "-u", "tools/ab_walk.py", ":".join(p[1:])], env
+    if kind == "abt":   # abt=TILE:REPS:CFGS:SPECS -- ab on rank 0's tile of a TILE-GPU run, REPS frames timed
+        env["AB_TILE"], env["AB_REPS"], env["AB_CFGS"] = p[0], p[1], p[2]
+        return [PY, "-u", "tools/ab_walk.py", ":".join(p[3:])], env
     if kind == "tiles":
         return [PY, "-u", "tools/occupancy_probe.py", p[0], p[1], p[2] if len(p) > 2 else ""], env
     if kind in ("kt", "pmc"):
@@ -90,6 +95,10 @@ def command(kind, val, tag, n):
             bench_args(cfg, nst or "1", "1", opts) + ["--no-counts"], env
     if kind == "py":
         return [PY, "-u", p[0]] + (p[1].split("+") if len(p) > 1 and p[1] else []), env
+    if kind == "pmcpy":   # pmcpy=NAME:GROUP:SCRIPT[:ARGS] -- one --pmc pass (GROUP as pmc=) of a py step
+        name = f"{tag}_pmc_{p[0]}_{p[1]}"
+        return ["rocprofv3", "--pmc"] + PMC[p[1]].split() + ["--output-format", "csv", "-d", os.path.join(OUT, name),
+                "-o", name, "--", PY, "-u", p[2]] + (p[3].split("+") if len(p) > 3 and p[3] else []), env
     if kind == "ktpy":
         name = f"{tag}_kt_{p[0]}"
         return ["rocprofv3", "--kernel-trace", "--stats", "--output-format", "csv", "-d", os.path.join(OUT, name),
