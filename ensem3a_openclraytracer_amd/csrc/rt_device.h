@@ -408,8 +408,6 @@ __device__ __forceinline__ ConstF4 as_const(const float4* p) {
     return ConstF4{(const const_f*)(const float*)(p)};   // C-style: an address-space cast
 }
 
-typedef float f32x2 __attribute__((ext_vector_type(2)));   // packed FP32 pairs (v_pk_add_f32 / v_pk_mul_f32)
-
 __device__ __forceinline__ float sgpr1(float x) {
     return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(x)));
 }
@@ -428,7 +426,11 @@ __device__ __forceinline__ float4 sgpr4(float4 v) {
 // (distance bits, DFS position): positive float bits order like the floats, so
 // the minimum key is the reference's hit (lowest rank on equal distances).
 // Culling uses the owner's best as of the last batch (a conservative bound).
+#if RT_BRUTE_FLATQ
+constexpr int BRUTE_WAVE_LDS = 64 * 6 * 4 + 64 * 8 + 320 * 4;   // ray table | best keys | pair ring + dummy slots
+#else
 constexpr int BRUTE_WAVE_LDS = 64 * 6 * 4 + 64 * 8 + 256 * 4;   // ray table | best keys | pair ring
+#endif
 
 // Lanes of one wave hand data to each other through LDS here.  The hardware runs a
 // wave's LDS instructions in order; this keeps the compiler from reordering them
@@ -502,12 +504,20 @@ __device__ Hit trace_brute_compact(const DevScene& S, rtm_f3 o, rtm_f3 d, char* 
         const unsigned long long m = __ballot(pass);
         if (m == 0) return;
         const unsigned n = (unsigned)__popcll(m);
+#if RT_BRUTE_FLATQ
+        // no exec-mask change: a lane that does not pass writes its entries to a private dummy slot
+        if (COUNT && pass) c.tris += qb >= 0 ? 2 : 1;
+        const unsigned r = lane_prefix(m, tail);
+        ring[pass ? (r & 255) : 256u + lane] = (tl << 16) | qa;
+        if (qb >= 0) ring[pass ? ((r + n) & 255) : 256u + lane] = (tl << 16) | (unsigned)qb;
+#else
         if (pass) {
             if (COUNT) c.tris += qb >= 0 ? 2 : 1;
             const unsigned r = lane_prefix(m, tail);
             ring[r & 255] = (tl << 16) | qa;
             if (qb >= 0) ring[(r + n) & 255] = (tl << 16) | (unsigned)qb;
         }
+#endif
         tail += qb >= 0 ? 2 * n : n;
         wave_lds_sync();
         if ((int)(tail - head) >= nact) {
@@ -521,57 +531,23 @@ __device__ Hit trace_brute_compact(const DevScene& S, rtm_f3 o, rtm_f3 d, char* 
         // to back, then the passes are queued (culling uses the best hit as of the group's start:
         // conservative)
         const ConstF4 cb = as_const(S.brute_box);
-#if RT_BRUTE_PK
-        // packed FP32: each axis's (lo, hi) pair (an aligned SGPR pair of the box record) in one
-        // v_pk_add_f32 and one v_pk_mul_f32 -- the same IEEE operations as slab()
-        const f32x2 o2x = {o.x, o.x}, o2y = {o.y, o.y}, o2z = {o.z, o.z};
-        const f32x2 i2x = {ix, ix}, i2y = {iy, iy}, i2z = {iz, iz};
-#endif
-#if RT_BRUTE_PREF
-        // the next group's scalar loads go out after this group's slab tests, while its passes are queued
-        float4 bx[2 * kBoxGroup];
-#pragma unroll
-        for (int j = 0; j < 2 * kBoxGroup; ++j) bx[j] = sgpr4(cb[j]);
-#endif
         for (int g0 = 0; g0 < S.nbox; g0 += kBoxGroup) {
-#if !RT_BRUTE_PREF
             float4 bx[2 * kBoxGroup];
 #pragma unroll
             for (int j = 0; j < 2 * kBoxGroup; ++j) bx[j] = sgpr4(cb[2 * g0 + j]);
-#endif
             const float cull = bk * CULL_MARGIN;
             bool pass[kBoxGroup];
 #pragma unroll
             for (int j = 0; j < kBoxGroup; ++j) {
                 float tn, tx;
-#if RT_BRUTE_PK
-                const f32x2 X = (f32x2{bx[2 * j].x, bx[2 * j].y} - o2x) * i2x;
-                const f32x2 Y = (f32x2{bx[2 * j].z, bx[2 * j].w} - o2y) * i2y;
-                const f32x2 Z = (f32x2{bx[2 * j + 1].x, bx[2 * j + 1].y} - o2z) * i2z;
-                tn = fmaxf(fmaxf(fminf(X.x, X.y), fminf(Y.x, Y.y)), fminf(Z.x, Z.y));
-                tx = fminf(fminf(fmaxf(X.x, X.y), fmaxf(Y.x, Y.y)), fmaxf(Z.x, Z.y));
-#else
                 slab(bx[2 * j].x, bx[2 * j].y, bx[2 * j].z, bx[2 * j].w, bx[2 * j + 1].x, bx[2 * j + 1].y, o, ix, iy,
                      iz, tn, tx);
-#endif
                 pass[j] = box_hit(tn, tx, cull);
             }
-            int qa_[kBoxGroup], qb_[kBoxGroup];
-#pragma unroll
-            for (int j = 0; j < kBoxGroup; ++j) {
-                qa_[j] = __float_as_int(bx[2 * j + 1].z);
-                qb_[j] = __float_as_int(bx[2 * j + 1].w);
-            }
-#if RT_BRUTE_PREF
-            if (g0 + kBoxGroup < S.nbox) {   // (brute_box is padded to whole groups)
-#pragma unroll
-                for (int j = 0; j < 2 * kBoxGroup; ++j) bx[j] = sgpr4(cb[2 * (g0 + kBoxGroup) + j]);
-            }
-#endif
 #pragma unroll
             for (int j = 0; j < kBoxGroup; ++j) {
                 if (g0 + j >= S.nbox) break;   // padding (never hit; skipped so the counters stay exact)
-                const int qa = qa_[j], qb = qb_[j];
+                const int qa = __float_as_int(bx[2 * j + 1].z), qb = __float_as_int(bx[2 * j + 1].w);
                 if (COUNT) {   // counted per record (one leaf box test each, as in the tree walk)
                     c.boxes++;
                     count_wave(c.wave_trav); c.nodes++;

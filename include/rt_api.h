@@ -74,8 +74,8 @@ int rt_set_scene(rt_ctx* ctx, const float* vp, int64_t nvp, const float* vn, int
 int rt_set_env(rt_ctx* ctx, const uint8_t* rgba, int w, int h);
 
 /* Integer options of the drop-in contract:
- *   "traversal"  rt_traversal (FAST default; REF = the reference's own DFS, stack.cl's 20 slots);
- *   "bvh"        rt_bvh_layout the FAST walk uses (SAH default) -- same hits;
+ *   "traversal"  an rt_traversal value: FAST (default) or REF = the reference's own DFS, stack.cl's 20 slots;
+ *   "bvh"        an rt_bvh_layout value: the tree the FAST walk uses, SAH by default -- same hits;
  *   "bvh_width"  FAST tree walk: 2 = BVH2 nodes, 4 = the 4-wide quantised layout, 0 = auto (4-wide when
  *                the BVH2 node array exceeds 16 MB) -- same frame;
  *   "brute_max"  FAST on scenes of at most this many triangles tests every leaf box in lock-step instead

@@ -16,6 +16,9 @@ export ENSEM3A_ORACLE_LIB="$ROOT/build/asan/liboracle_asan.so"
 # leaks: python's own allocations are not ours to report; new/delete and malloc/free mismatches are
 export ASAN_OPTIONS="detect_leaks=0:halt_on_error=1:abort_on_error=1:detect_odr_violation=0:alloc_dealloc_mismatch=1"
 export UBSAN_OPTIONS="halt_on_error=1:print_stacktrace=1"
+# --capture=sys: pytest captures python-level output only, so a sanitizer report (written to fd 2 by the
+# native runtime just before it aborts the process) reaches the terminal instead of a discarded capture file
 if [ "$#" -eq 0 ]; then set -- tests -m "not gpu" -x -q -p no:cacheprovider; fi
+set -- --capture=sys "$@"
 cd "$ROOT"
 LD_PRELOAD="$ASAN_RT $UBSAN_RT" python -m pytest "$@"
