@@ -36,6 +36,8 @@ def build_export_array(faceData, V_p) -> np.ndarray:
                                  "(triangles with identical centroids)")
     if st == 2:
         raise ValueError("faceData position index out of range")
+    if st == 4:
+        raise MemoryError("rt_bvh_build: out of host memory")
     if st != 0:
         raise ValueError(f"rt_bvh_build failed with status {st}")
     return out[: 9 * nodes.value]

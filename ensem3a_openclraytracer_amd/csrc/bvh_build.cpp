@@ -24,6 +24,7 @@
 #include <cmath>
 #include <vector>
 #include <algorithm>
+#include <new>
 
 namespace {
 
@@ -39,10 +40,23 @@ struct BuildNode {
 extern "C" {
 
 // Returns 0 on success; 1 bad arguments; 2 index out of range; 3 degenerate
-// split (reference would not terminate).  out must hold 9*(2T-1) floats
+// split (reference would not terminate); 4 out of host memory.  out must hold 9*(2T-1) floats
 // (T = nface/10); *out_nodes receives the node count actually written.
+static int bvh_build(const int32_t* face, int64_t nface, const float* vp, int64_t nvp, float* out,
+                     int64_t* out_nodes);
+
+// No C++ exception leaves the C ABI: 4 = out of host memory.
 int rt_bvh_build(const int32_t* face, int64_t nface, const float* vp, int64_t nvp,
                  float* out, int64_t* out_nodes) {
+    try {
+        return bvh_build(face, nface, vp, nvp, out, out_nodes);
+    } catch (const std::bad_alloc&) {
+        return 4;
+    }
+}
+
+static int bvh_build(const int32_t* face, int64_t nface, const float* vp, int64_t nvp, float* out,
+                     int64_t* out_nodes) {
     if (!face || !vp || !out || !out_nodes || nface < 0 || nface % 10 != 0 || nvp % 3 != 0)
         return 1;
     const int64_t T = nface / 10;

@@ -18,6 +18,7 @@
 #include <cstring>
 #include <limits>
 #include <numeric>
+#include <system_error>
 #include <thread>
 #include <vector>
 
@@ -268,7 +269,13 @@ void sah_build(const float* leaf_boxes, const int32_t* leaf_ids, int64_t n, SahT
             }
         };
         std::vector<std::thread> pool;
-        for (unsigned t = 1; t < hw; ++t) pool.emplace_back(worker);
+        for (unsigned t = 1; t < hw; ++t) {
+            try {
+                pool.emplace_back(worker);
+            } catch (const std::system_error&) {   // no more threads: the ones started do the rest
+                break;
+            }
+        }
         worker();
         for (auto& t : pool) t.join();
         // stitch: subtree k's node 0 becomes the deferred node, its other nodes are appended

@@ -18,6 +18,8 @@
 #include <cstdint>
 #include <cstdlib>
 #include <cstring>
+#include <memory>
+#include <new>
 #include <string>
 #include <vector>
 
@@ -92,10 +94,21 @@ extern "C" {
 
 const char* rt_obj_last_error(void) { return g_obj_error.c_str(); }
 
+static int obj_parse(const char* text, int64_t len, rt_obj** out);
+
+// No C++ exception leaves the C ABI: a file too large for host memory is a parse failure.
 int rt_obj_parse(const char* text, int64_t len, rt_obj** out) {
+    try {
+        return obj_parse(text, len, out);
+    } catch (const std::bad_alloc&) {
+        return fail("out of host memory");
+    }
+}
+
+static int obj_parse(const char* text, int64_t len, rt_obj** out) {
     if (!out || (!text && len > 0) || len < 0) return fail("bad arguments");
     *out = nullptr;
-    rt_obj* o = new rt_obj();
+    std::unique_ptr<rt_obj> o(new rt_obj());   // freed on every failure path, and on bad_alloc
     std::vector<std::pair<const char*, const char*>> ws;
     bool seen_usemtl = false;
     const char* p = text;
@@ -113,11 +126,10 @@ int rt_obj_parse(const char* text, int64_t len, rt_obj** out) {
             const bool is_vn = hl == 2 && hp[0] == 'v' && hp[1] == 'n';
             const bool is_vt = hl == 2 && hp[0] == 'v' && hp[1] == 't';
             if (is_v || is_vn) {
-                if (ws.size() < 4) { delete o; return fail("line " + std::to_string(lineno) + ": short vertex"); }
+                if (ws.size() < 4) { return fail("line " + std::to_string(lineno) + ": short vertex"); }
                 for (int k = 1; k <= 3; ++k) {
                     double v;
                     if (!parse_float(ws[k].first, ws[k].second, &v)) {
-                        delete o;
                         return fail("line " + std::to_string(lineno) + ": bad number");
                     }
                     (is_v ? o->vp : o->vn).push_back((float)v);
@@ -126,7 +138,6 @@ int rt_obj_parse(const char* text, int64_t len, rt_obj** out) {
                 double u = 0.0, v = 0.0;
                 if (ws.size() < 2 || !parse_float(ws[1].first, ws[1].second, &u) ||
                     (ws.size() > 2 && !parse_float(ws[2].first, ws[2].second, &v))) {
-                    delete o;
                     return fail("line " + std::to_string(lineno) + ": bad texture coordinate");
                 }
                 o->vuv.push_back((float)u);
@@ -155,7 +166,7 @@ int rt_obj_parse(const char* text, int64_t len, rt_obj** out) {
                 if (!sp) break;
                 q = sp + 1;
             }
-            if (nf < 4) { delete o; return fail("line " + std::to_string(lineno) + ": face with fewer than 3 vertices"); }
+            if (nf < 4) { return fail("line " + std::to_string(lineno) + ": face with fewer than 3 vertices"); }
             int32_t row[10];
             row[0] = (int32_t)o->mat_counter;
             const int comps[3] = {1, 2, 0};   // uv, normal, position
@@ -167,19 +178,17 @@ int rt_obj_parse(const char* text, int64_t len, rt_obj** out) {
                     const char* fe = fends[j];
                     for (int skip = 0; skip < comps[ci]; ++skip) {
                         const char* sl = static_cast<const char*>(std::memchr(s, '/', (size_t)(fe - s)));
-                        if (!sl) { delete o; return fail("line " + std::to_string(lineno) + ": face vertex without uv/normal"); }
+                        if (!sl) { return fail("line " + std::to_string(lineno) + ": face vertex without uv/normal"); }
                         s = sl + 1;
                     }
                     const char* sl = static_cast<const char*>(std::memchr(s, '/', (size_t)(fe - s)));
                     long long v;
                     if (!parse_int(s, sl ? sl : fe, &v)) {
-                        delete o;
                         return fail("line " + std::to_string(lineno) + ": bad face index");
                     }
                     // the reference stores faceData as int32 (FileManager.py:276-282): an index it cannot hold
                     // is refused here rather than wrapped
                     if (v - 1 < INT32_MIN || v - 1 > INT32_MAX) {
-                        delete o;
                         return fail("line " + std::to_string(lineno) + ": face index out of the int32 range");
                     }
                     row[w++] = (int32_t)(v - 1);
@@ -191,7 +200,7 @@ int rt_obj_parse(const char* text, int64_t len, rt_obj** out) {
         }
         p = le;
     }
-    *out = o;
+    *out = o.release();
     return 0;
 }
 

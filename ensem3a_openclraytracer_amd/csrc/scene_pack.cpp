@@ -11,7 +11,10 @@
 #include <atomic>
 #include <map>
 #include <mutex>
+#include <new>
+#include <stdexcept>
 #include <string>
+#include <system_error>
 #include <thread>
 #include <vector>
 
@@ -64,7 +67,13 @@ void parallel_for(int64_t n, int64_t grain, F f) {
         for (int64_t k; (k = next.fetch_add(1)) < chunks;) f(k * grain, std::min(n, (k + 1) * grain));
     };
     std::vector<std::thread> pool;
-    for (int t = 1; t < nt; ++t) pool.emplace_back(run);
+    for (int t = 1; t < nt; ++t) {
+        try {
+            pool.emplace_back(run);
+        } catch (const std::system_error&) {   // no more threads: the ones started (and this one) do the rest
+            break;
+        }
+    }
     run();
     for (auto& t : pool) t.join();
 }
@@ -560,9 +569,11 @@ void pack_checked(HostScene& hs, const float* bvh9, int64_t nb, int64_t ntri, in
     if (hs.brute_box.empty()) hs.brute_box.assign(8 * rt::kBoxGroup, 1e30f);
 }
 
-int scene_prepare(HostScene& hs, const float* vp, int64_t nvp, const float* vn, int64_t nvn, const int32_t* face,
-                  int64_t nface, const float* mat, int64_t nmat, const float* bvh9, int64_t nbvh, int layout,
-                  int brute_max, std::string& msg, std::string& why) {
+namespace {
+
+int scene_prepare_(HostScene& hs, const float* vp, int64_t nvp, const float* vn, int64_t nvn, const int32_t* face,
+                   int64_t nface, const float* mat, int64_t nmat, const float* bvh9, int64_t nbvh, int layout,
+                   int brute_max, std::string& msg, std::string& why) {
     if (nvp < 0 || nvp % 3 || nvn < 0 || nvn % 3 || nface < 0 || nface % 10 || nmat <= 0 || nmat % 6 || nbvh < 0 ||
         nbvh % 9)
         return fail(msg, RT_ERR_ARG,
@@ -641,6 +652,23 @@ int scene_prepare(HostScene& hs, const float* vp, int64_t nvp, const float* vn, 
     }
     pack_checked(hs, bvh9, NB, T, layout, brute_max, why);
     return RT_OK;
+}
+
+}  // namespace
+
+// No C++ exception leaves the C ABI: a scene too large for host memory is an error status.
+int scene_prepare(HostScene& hs, const float* vp, int64_t nvp, const float* vn, int64_t nvn, const int32_t* face,
+                  int64_t nface, const float* mat, int64_t nmat, const float* bvh9, int64_t nbvh, int layout,
+                  int brute_max, std::string& msg, std::string& why) {
+    try {
+        return scene_prepare_(hs, vp, nvp, vn, nvn, face, nface, mat, nmat, bvh9, nbvh, layout, brute_max, msg, why);
+    } catch (const std::bad_alloc&) {
+        hs = HostScene();
+        return fail(msg, RT_ERR_ARG, "scene too large for host memory");
+    } catch (const std::exception& e) {
+        hs = HostScene();
+        return fail(msg, RT_ERR_ARG, "scene preparation failed: %s", e.what());
+    }
 }
 
 }  // namespace rt
