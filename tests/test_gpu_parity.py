@@ -614,6 +614,46 @@ def test_error_behaviour(kl):
     fresh.close()
 
 
+def test_scene_check_agrees_with_set_scene(kl):
+    """rt_scene_check (host only) returns the status rt_set_scene returns on the same arrays, and the layout
+    it packs is the one the context uploads; rt_debug_timings records the calls' host times."""
+    sc = W.load_scene("cornell")
+    base = (sc.V_p, sc.V_n, sc.faceData, sc.materialData, sc.BVH.exportArray)
+    cyc = sc.BVH.exportArray.copy().reshape(-1, 9)
+    cyc[1, 0] = 0
+    mat = sc.materialData.copy()
+    mat[0] = 5.0
+    face = sc.faceData.copy()
+    face[7] = 10 ** 6
+    cases = [base, (sc.V_p, sc.V_n, sc.faceData, sc.materialData, cyc.reshape(-1)),
+             (sc.V_p, sc.V_n, sc.faceData, mat, sc.BVH.exportArray), (sc.V_p, sc.V_n, face, sc.materialData,
+                                                                       sc.BVH.exportArray)]
+    ctx = _native.Context()
+    try:
+        for vp, vn, f, m, b in cases:
+            try:
+                _native.scene_check(vp, vn, f, m, b)
+                want = 0
+            except _native.NativeError as e:
+                want = e.status
+            try:
+                ctx.set_scene(vp, vn, sc.V_uv, f, m, b)
+                got = 0
+            except _native.NativeError as e:
+                got = e.status
+            assert got == want
+        ctx.set_scene(sc.V_p, sc.V_n, sc.V_uv, sc.faceData, sc.materialData, sc.BVH.exportArray)
+        info, chk = ctx.scene_info(), _native.scene_check(*base)
+        assert (info["nodes"], info["tris"], info["brute_records"], info["brute_boxes"], info["depth"]) == \
+            (chk["nodes"], chk["tris"], chk["brute_records"], chk["brute_boxes"], chk["depth"])
+        ctx.set_env(W.ibl_preview())
+        ctx.render(sc.camera(16, 16), sc.env(), 256, 2, 4)
+        tm = ctx.timings()
+        assert tm["pack_ms"] >= 0 and tm["upload_ms"] > 0 and tm["env_ms"] > 0 and tm["render_ms"] > 0, tm
+    finally:
+        ctx.close()
+
+
 def test_material_change_invalidates_cached_upload(kl):
     wl = W.PARITY_CASES["cornell_64_s4"]
     sc, cam, env, npix, spp, mb, ibl = wl.inputs()
