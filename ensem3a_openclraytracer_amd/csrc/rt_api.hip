@@ -53,6 +53,7 @@ struct Device {
     DevBuf spec;                  // speculation: the trails' sample logs (FrameParams::spec_log)
     DevBuf slice;                 // sample slices: per-pixel state + samples done (FrameParams::slice_*)
     char* host_stage = nullptr;   // pinned staging for rt_render / rt_render_rgb8
+    int* host_pick = nullptr;     // pinned: a two-pass launch's pass-2 pick, read back (rt::RenderPending)
     size_t host_stage_bytes = 0;
     // Every launch of this context on the device shares `work` (pixel counters + launch constants)
     // and reads the scene buffers, so launches are ordered across streams: `done` is recorded after
@@ -330,6 +331,7 @@ void rt_destroy(rt_ctx* ctx) {
                           &d.out8, &d.counts, &d.work, &d.scratch_a, &d.scratch_b, &d.pilot, &d.spec, &d.slice})
             release(*b);
         if (d.host_stage) (void)hipHostFree(d.host_stage);
+        if (d.host_pick) (void)hipHostFree(d.host_pick);
         if (d.stream) (void)hipStreamDestroy(d.stream);
         if (d.done) (void)hipEventDestroy(d.done);
     }
@@ -758,7 +760,10 @@ int render_host_(rt_ctx* ctx, const float cam[10], const float env[5], int64_t n
     const int nd = (int)ctx->devs.size();
     const int W = fp0.width;
     const size_t elem = rgb8 >= 0 ? 1 : sizeof(float);
-    // Launch every device, then read back: devices run concurrently.
+    // Launch every device, then read back: devices run concurrently.  A two-pass launch's second pass
+    // waits for the device's pick after its first pass (rt::RenderPending): every device's first pass is
+    // enqueued before the host waits for any.
+    std::vector<rt::RenderPending> pend(nd);
     for (int k = 0; k < nd; ++k) {
         Device& d = ctx->devs[k];
         rt::FrameParams fp = fp0;
@@ -780,14 +785,26 @@ int render_host_(rt_ctx* ctx, const float cam[10], const float env[5], int64_t n
         HIP_OR_RET(ctx, order_after_last(d, d.stream));
         HIP_OR_RET(ctx, setup_pilot(ctx, d, fp));
         HIP_OR_RET(ctx, setup_slices(ctx, d, fp, d.stream));
+        if (!d.host_pick) HIP_OR_RET(ctx, hipHostMalloc((void**)&d.host_pick, sizeof(int), hipHostMallocDefault));
+        pend[k].host_pick = d.host_pick;
         HIP_OR_RET(ctx, rt::launch_render(dev_scene(ctx, d), fp, effective_traversal(ctx), ctx->block,
-                                          (float*)d.out.p, nullptr, (unsigned int*)d.work.p, d.stream));
+                                          (float*)d.out.p, nullptr, (unsigned int*)d.work.p, d.stream, &pend[k]));
+        HIP_OR_RET(ctx, mark_launch(d, d.stream));   // (again after pass 2 below; an error in between leaves it ordered)
+    }
+    for (int k = 0; k < nd; ++k) {
+        Device& d = ctx->devs[k];
+        const int64_t nloc = rt_tile_rows(npix, W, k, nd) * W;
+        const size_t bytes = (size_t)nloc * 3 * elem;
+        if (bytes == 0) continue;
+        HIP_OR_RET(ctx, hipSetDevice(d.id));
+        HIP_OR_RET(ctx, rt::launch_render_finish(dev_scene(ctx, d), effective_traversal(ctx), ctx->block,
+                                                 (float*)d.out.p, (unsigned int*)d.work.p, d.stream, pend[k]));
         HIP_OR_RET(ctx, mark_launch(d, d.stream));
         const void* src = d.out.p;
         if (rgb8 >= 0) {
             HIP_OR_RET(ctx, ensure(d.out8, bytes));
-            HIP_OR_RET(ctx, rt::launch_rgb8((const float*)d.out.p, (uint8_t*)d.out8.p, (int64_t)fp.nloc * 3,
-                                            rgb8 == 1, d.stream));
+            HIP_OR_RET(ctx, rt::launch_rgb8((const float*)d.out.p, (uint8_t*)d.out8.p, nloc * 3, rgb8 == 1,
+                                            d.stream));
             src = d.out8.p;
         }
         HIP_OR_RET(ctx, hipMemcpyAsync(d.host_stage, src, bytes, hipMemcpyDeviceToHost, d.stream));

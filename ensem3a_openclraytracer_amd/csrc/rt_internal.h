@@ -134,11 +134,25 @@ struct FrameParams {
     int32_t* log_count;
 };
 
+// A two-pass launch's second pass, waiting for the first: pass 2 launches the kernel the device picked
+// (pilot_team_pick_kernel) from the pixels pass 1 left, so the host reads that pick back first.
+// launch_render with a RenderPending stops once the pick's copy into pinned host memory is enqueued;
+// launch_render_finish waits for it and launches pass 2 (render_host starts every device before it
+// waits for any).  Without one, launch_render waits itself.
+struct RenderPending {
+    bool pick = false;        // pass 2 still to launch
+    int* host_pick = nullptr; // pinned host int (the caller's)
+    FrameParams b{};          // pass 2's parameters
+    bool spec_ok = false;
+};
 // Launch the render kernel; counts != nullptr selects the instrumented build
 // (device pointer to 5 uint64 accumulators).
 // d_work: kWorkBytes of device scratch (layout above; the counters are zeroed by the launch).
 hipError_t launch_render(const DevScene& sc, const FrameParams& fp, int traversal, int block,
-                         float* d_out, unsigned long long* d_counts, unsigned int* d_work, hipStream_t stream);
+                         float* d_out, unsigned long long* d_counts, unsigned int* d_work, hipStream_t stream,
+                         RenderPending* pend = nullptr);
+hipError_t launch_render_finish(const DevScene& sc, int traversal, int block, float* d_out, unsigned int* d_work,
+                                hipStream_t stream, RenderPending& pend);
 hipError_t launch_prep_frames(const DevScene& sc, float4* frame, hipStream_t stream);
 // the IBL's 2x2 texel-sum table (DevScene::ibl_sum) from the RGBA8 image: (w + 1) x (h + 1) words
 hipError_t launch_ibl_sum(const uchar4* rgba, int w, int h, uint32_t* sum, hipStream_t stream);

@@ -1231,7 +1231,7 @@ hipError_t launch_render_pass(const DevScene& sc, const FrameParams& fp, int tra
 // frame ends when its last-started pixels finish; started last, the cheapest pixels make that tail
 // short.  Every pixel's samples run in the same order as in one pass, so the frame is bit-identical.
 hipError_t launch_render(const DevScene& sc, const FrameParams& fp, int traversal, int block, float* d_out,
-                         unsigned long long* d_counts, unsigned int* d_work, hipStream_t stream) {
+                         unsigned long long* d_counts, unsigned int* d_work, hipStream_t stream, RenderPending* pend) {
     if (fp.pilot <= 0 || fp.pass != 0 || d_counts || fp.spp <= fp.pilot || fp.nloc <= 0 || !fp.pilot_state)
         return launch_render_pass(sc, fp, traversal, block, d_out, d_counts, d_work, stream);
     FrameParams a = fp;
@@ -1288,16 +1288,37 @@ hipError_t launch_render(const DevScene& sc, const FrameParams& fp, int traversa
                            (int64_t)std::max(cus, 1) * kWalkLanesPerCu, spec_ok ? 1 : 0, ts);
         // the pick is read back (pass 1 has to finish before pass 2 anyway) and exactly the kernel it names
         // is launched: 1, 2 or 4 lanes per pixel, or kSpecPick + T trails
-        int pick = 1;
-        e = hipMemcpyAsync(&pick, ts, sizeof(int), hipMemcpyDeviceToHost, stream);
-        if (e == hipSuccess) e = hipStreamSynchronize(stream);
-        if (e != hipSuccess) return e;
-        if (spec_ok && pick > kSpecPick) {
-            b.spec = pick - kSpecPick;
-            return launch_spec(sc, b, block, d_out, d_work, stream);
+        RenderPending local;
+        RenderPending& P = pend ? *pend : local;
+        int pick_stack = 1;
+        if (!P.host_pick) {
+            if (pend) return hipErrorInvalidValue;   // a deferred pass 2 needs the caller's (pinned) int
+            P.host_pick = &pick_stack;               // pageable: this call waits itself
         }
-        b.walk_team = pick;
+        e = hipMemcpyAsync(P.host_pick, ts, sizeof(int), hipMemcpyDeviceToHost, stream);
+        if (e != hipSuccess) return e;
+        P.pick = true;
+        P.b = b;
+        P.spec_ok = spec_ok;
+        if (pend) return hipSuccess;
+        return launch_render_finish(sc, traversal, block, d_out, d_work, stream, P);
     }
+    return launch_render_pass(sc, b, traversal, block, d_out, nullptr, d_work, stream);
+}
+
+hipError_t launch_render_finish(const DevScene& sc, int traversal, int block, float* d_out, unsigned int* d_work,
+                                hipStream_t stream, RenderPending& P) {
+    if (!P.pick) return hipSuccess;
+    P.pick = false;
+    hipError_t e = hipStreamSynchronize(stream);
+    if (e != hipSuccess) return e;
+    const int pick = *P.host_pick;
+    FrameParams b = P.b;
+    if (P.spec_ok && pick > kSpecPick) {
+        b.spec = pick - kSpecPick;
+        return launch_spec(sc, b, block, d_out, d_work, stream);
+    }
+    b.walk_team = pick;
     return launch_render_pass(sc, b, traversal, block, d_out, nullptr, d_work, stream);
 }
 
