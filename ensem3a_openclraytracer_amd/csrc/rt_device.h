@@ -426,7 +426,8 @@ __device__ __forceinline__ float4 sgpr4(float4 v) {
 // (distance bits, DFS position): positive float bits order like the floats, so
 // the minimum key is the reference's hit (lowest rank on equal distances).
 // Culling uses the owner's best as of the last batch (a conservative bound).
-constexpr int BRUTE_WAVE_LDS = 64 * 6 * 4 + 64 * 8 + 320 * 4;   // ray table | best keys | pair ring + dummy slots
+constexpr unsigned BRUTE_RING = 256u;
+constexpr int BRUTE_WAVE_LDS = 64 * 6 * 4 + 64 * 8 + (BRUTE_RING + 64) * 4;   // ray table | best keys | pair ring + dummy slots
 
 // Lanes of one wave hand data to each other through LDS here.  The hardware runs a
 // wave's LDS instructions in order; this keeps the compiler from reordering them
@@ -469,7 +470,7 @@ __device__ Hit trace_brute_compact(const DevScene& S, rtm_f3 o, rtm_f3 d, char* 
     unsigned head = 0, tail = 0;   // wave-uniform ring positions
     auto run_batch = [&](int n) __attribute__((always_inline)) {
         if (myrank < n) {
-            const unsigned e = ring[(head + myrank) & 255];
+            const unsigned e = ring[(head + myrank) & (BRUTE_RING - 1)];
             const unsigned ow = e >> 16, q = e & 0xffffu;
             const rtm_f3 ro = rtm_v3(ray[ow], ray[64 + ow], ray[128 + ow]);
             const rtm_f3 rd = rtm_v3(ray[192 + ow], ray[256 + ow], ray[320 + ow]);
@@ -504,8 +505,8 @@ __device__ Hit trace_brute_compact(const DevScene& S, rtm_f3 o, rtm_f3 d, char* 
         // the ring (r06: the 1/8 tile 2.25 -> 2.19 ms, the whole frame unchanged)
         if (COUNT && pass) c.tris += qb >= 0 ? 2 : 1;
         const unsigned r = lane_prefix(m, tail);
-        ring[pass ? (r & 255) : 256u + lane] = (tl << 16) | qa;
-        if (qb >= 0) ring[pass ? ((r + n) & 255) : 256u + lane] = (tl << 16) | (unsigned)qb;
+        ring[pass ? (r & (BRUTE_RING - 1)) : BRUTE_RING + lane] = (tl << 16) | qa;
+        if (qb >= 0) ring[pass ? ((r + n) & (BRUTE_RING - 1)) : BRUTE_RING + lane] = (tl << 16) | (unsigned)qb;
         tail += qb >= 0 ? 2 * n : n;
         wave_lds_sync();
         if ((int)(tail - head) >= nact) {
@@ -534,7 +535,10 @@ __device__ Hit trace_brute_compact(const DevScene& S, rtm_f3 o, rtm_f3 d, char* 
             }
 #pragma unroll
             for (int j = 0; j < kBoxGroup; ++j) {
-                if (g0 + j >= S.nbox) break;   // padding (never hit; skipped so the counters stay exact)
+                // padding boxes (a point at 1e30: every slab distance is beyond the cull or behind the ray) never
+                // pass, so the product build queues nothing for them without a check (r06: the 1/8 tile 2.19 ->
+                // 2.16 ms, the frame unchanged); the instrumented build skips them so the counters stay exact
+                if (COUNT && g0 + j >= S.nbox) break;
                 const int qa = __float_as_int(bx[2 * j + 1].z), qb = __float_as_int(bx[2 * j + 1].w);
                 if (COUNT) {   // counted per record (one leaf box test each, as in the tree walk)
                     c.boxes++;
@@ -1145,6 +1149,68 @@ __device__ __forceinline__ bool fast_step_pipe(FastRay& R, ItemData& D, const ch
     R.brank = take ? rank : R.brank;
     R.item = done ? R.item : next;
     return done | (take & R.any);
+}
+
+// ---- top levels of the BVH2 tree from scalar loads (RT_TOP_LEVELS = 1: the root; 2: and its children) ----
+// The first node steps of a ray that has just started at the root run here for every such lane of
+// the wave at once, with the node read through scalar loads (one record per wave, SGPR operands,
+// no vector memory instruction): the root, then (RT_TOP_LEVELS = 2) each of its two internal
+// children for the lanes whose walk continues into it.  The arithmetic, push order and cull are
+// fast_step_pipe's node part, so the walk that follows is the one the item steps would have made.
+// Returns false when the ray is finished (every box missed).  r06 (profiles/r06_ab_top_levels_ta.json):
+// the root alone C3 107.4 / 107.3 -> 107.1 / 106.6 ms, C4 272.2 / 269.6 -> 270.1 / 267.4 ms (kept); with
+// its children vector-memory reads -5.4 % (C3) / -1.8 % (C4) but C3 108.8-109.1 ms, C4 270.8-273.4 ms.
+#ifndef RT_TOP_LEVELS
+#define RT_TOP_LEVELS 1
+#endif
+template <bool COUNT, bool OVF>
+__device__ __forceinline__ void top_node_step(const const_f* n, bool on, FastRay& R, const LaneStack& st,
+                                              int& next, Cnt& c) {
+    const float4 g0 = sgpr4(make_float4(n[0], n[1], n[2], n[3]));
+    const float4 g1 = sgpr4(make_float4(n[4], n[5], n[6], n[7]));
+    const float4 g2 = sgpr4(make_float4(n[8], n[9], n[10], n[11]));
+    const int ex = __builtin_amdgcn_readfirstlane(__float_as_int(n[12]));
+    const int ey = __builtin_amdgcn_readfirstlane(__float_as_int(n[13]));
+    if (!on) return;
+    if (COUNT) { count_wave(c.wave_trav); c.nodes++; c.boxes += 2; }
+    const float cull = R.bk * CULL_MARGIN;
+    float t0n, t0x, t1n, t1x;
+    slab(g0.x, g0.y, g0.z, g0.w, g2.x, g2.y, R.o, R.ix, R.iy, R.iz, t0n, t0x);
+    slab(g1.x, g1.y, g1.z, g1.w, g2.z, g2.w, R.o, R.ix, R.iy, R.iz, t1n, t1x);
+    const bool h0 = box_hit(t0n, t0x, cull), h1 = box_hit(t1n, t1x, cull);
+    const bool first0 = t0n <= t1n;
+    if (h0 && h1) {
+        st.template put<OVF>(R.soff, make_int2(first0 ? ey : ex, __float_as_int(first0 ? t1n : t0n)));
+        R.soff += st.stride;
+    }
+    next = (h0 && h1) ? (first0 ? ex : ey) : h0 ? ex : h1 ? ey : INT_MIN;
+    if (next == INT_MIN) {   // the pop of fast_step_pipe (cull as of this step)
+        while (R.soff > 0) {
+            R.soff -= st.stride;
+            const int2 en = st.template get<OVF>(R.soff);
+            if (__int_as_float(en.y) <= cull) { next = en.x; break; }
+        }
+    }
+}
+// nb: the AoS node array (global memory); fresh: this lane's ray starts at the root this round
+template <bool COUNT, bool OVF>
+__device__ __forceinline__ bool top_levels(const DevScene& S, FastRay& R, bool fresh, const char* nb,
+                                           const LaneStack& st, Cnt& c) {
+    const int root = S.root_ref;
+    int next = R.item;
+    const const_f* cn = (const const_f*)(const float*)nb;
+    top_node_step<COUNT, OVF>(cn + 16 * root, fresh, R, st, next, c);
+    // the root's two children, each for the lanes whose walk went on into it
+    const int ex = __builtin_amdgcn_readfirstlane(__float_as_int(cn[16 * root + 12]));
+    const int ey = __builtin_amdgcn_readfirstlane(__float_as_int(cn[16 * root + 13]));
+    const bool on_x = fresh && ex >= 0 && next == ex, on_y = fresh && ey >= 0 && next == ey;
+    if (RT_TOP_LEVELS >= 2) {
+        if (ex >= 0 && __ballot(on_x)) top_node_step<COUNT, OVF>(cn + 16 * ex, on_x, R, st, next, c);
+        if (ey >= 0 && __ballot(on_y)) top_node_step<COUNT, OVF>(cn + 16 * ey, on_y, R, st, next, c);
+    }
+    if (!fresh) return true;
+    R.item = next;
+    return next != INT_MIN;
 }
 
 // ---- team traversal: TS lanes walk one ray (tiles with about one pixel per lane, option "walk_team") ----

@@ -775,6 +775,11 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WIDE ?
         // for the first step of this round are issued here (a lane continuing its ray re-fetches its item)
         constexpr bool PIPE = STEP && !WIDE && TS == 1;
         ItemData D;
+        if (RT_TOP_LEVELS && PIPE && !SMEM && S.root_ref >= 0) {
+            // rays started this round (still at the root: a started ray steps at least once per round)
+            const bool fresh = tracing && T.item == S.root_ref;
+            if (__ballot(fresh) && !top_levels<COUNT, OVF>(S, T, fresh, nb, lst, c)) tracing = false;
+        }
         if (PIPE && tracing) D = item_fetch<SMEM>(T.item, nb, tb, kstride);
         while (true) {
             if (tracing && (PIPE ? fast_step_pipe<COUNT, SMEM, OVF>(T, D, nb, tb, lst, kstride, c)

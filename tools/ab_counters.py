@@ -67,8 +67,14 @@ def main():
                     "valu_issue_frac": round(stall["SQ_INSTS_VALU"] * 64 / t2 / PEAK, 4),
                     "per_frame": {k: stall[k] / frames for k in ("SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_LDS")},
                 }
+            if ta:
+                row["ta_busy_frac"] = round(ta["TA_TA_BUSY_sum"] / (32 * ta["GRBM_GUI_ACTIVE"]), 4)
+                row["vmem_rd_per_frame"] = ta["SQ_INSTS_VMEM_RD"] / frames
+                row["valu_per_frame"] = ta["SQ_INSTS_VALU"] / frames
+                _, tt, _ = sums(os.path.join(ROOT, "gpurun_out", f"{sess}_pmc_{c}_ta{suf}"))
+                row["ta_pass_kernel_ms"] = round(tt / frames * 1e3, 3)
             if not sq:
-                if stall:
+                if stall or ta:
                     res["rows"][f"{name} {c}"] = row
                 continue
             row["dispatches"] = nd
@@ -77,9 +83,6 @@ def main():
             row["valu_lane_util"] = round(sq["SQ_THREAD_CYCLES_VALU"] / (64 * sq["SQ_ACTIVE_INST_VALU"]), 4)
             row["wait_frac"] = round(sq["SQ_WAIT_ANY"] / sq["SQ_WAVE_CYCLES"], 4)
             row["SQ_INSTS_VALU_per_frame"] = sq["SQ_INSTS_VALU"] / frames
-            if ta:
-                row["ta_busy_frac"] = round(ta["TA_TA_BUSY_sum"] / (32 * ta["GRBM_GUI_ACTIVE"]), 4)
-                row["vmem_rd_per_frame"] = ta["SQ_INSTS_VMEM_RD"] / frames
             res["rows"][f"{name} {c}"] = row
     with open(out, "w") as f:
         json.dump(res, f, indent=1)

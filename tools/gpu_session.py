@@ -23,6 +23,8 @@ STEP forms (values after '=' separated by ':'):
   py=SCRIPT[:ARGS]              python3 -u SCRIPT ARGS (ARGS split on '+')
   ktpy=NAME:SCRIPT[:ARGS]       rocprofv3 --kernel-trace --stats of a py step -> gpurun_out/TAG_kt_NAME
   pmcpy=NAME:GROUP:SCRIPT[:ARGS] one rocprofv3 --pmc pass of a py step -> gpurun_out/TAG_pmc_NAME_GROUP
+  lib=NAME                      later steps load lib/variants/libNAME.so (ENSEM3A_RT_LIB; kt / pmc output names
+                                get _NAME); lib=default goes back to the product library
 Limits: LIMIT_<KIND> env overrides the default seconds of a step kind.
 """
 import os
@@ -88,8 +90,10 @@ def command(kind, val, tag, n):
         cfg = p[0]
         opts = (p[2] if len(p) > 2 else "") if kind == "pmc" else (p[1] if len(p) > 1 else "")
         nst = (p[3] if len(p) > 3 else "1") if kind == "pmc" else (p[2] if len(p) > 2 else "1")
+        lib = os.environ.get("ENSEM3A_RT_LIB")
         name = f"{tag}_{kind}_{cfg}" + (f"_{p[1]}" if kind == "pmc" else "") + \
-            ("_" + "".join(ch if ch.isalnum() else "-" for ch in opts) if opts else "")
+            ("_" + "".join(ch if ch.isalnum() else "-" for ch in opts) if opts else "") + \
+            ("_" + os.path.basename(lib)[3:-3] if lib else "")
         prof = ["rocprofv3"] + (["--kernel-trace", "--stats"] if kind == "kt" else ["--pmc"] + PMC[p[1]].split())
         return prof + ["--output-format", "csv", "-d", os.path.join(OUT, name), "-o", name, "--"] + \
             bench_args(cfg, nst or "1", "1", opts) + ["--no-counts"], env
@@ -112,6 +116,14 @@ def main():
     os.environ.setdefault("TMPDIR", "/tmp")
     for n, st in enumerate(steps):
         kind, _, val = st.partition("=")
+        if kind == "lib":   # lib=NAME: later steps load lib/variants/libNAME.so (lib=default: the product library)
+            if val == "default":
+                os.environ.pop("ENSEM3A_RT_LIB", None)
+            else:
+                os.environ["ENSEM3A_RT_LIB"] = os.path.join(ROOT, "ensem3a_openclraytracer_amd", "lib", "variants",
+                                                            f"lib{val}.so")
+            print(f"== step {n}: {st}", flush=True)
+            continue
         cmd, env = command(kind, val, tag, n)
         limit = int(os.environ.get("LIMIT_" + kind.upper(), LIMITS[kind]))
         log = os.path.join(OUT, f"{tag}_{n}_{kind}.log")
