@@ -40,7 +40,10 @@ template <int TRAV, bool COUNT, bool LOG = false, bool SMEM = false, bool OVF = 
 // amdgpu_waves_per_eu(5): the register allocator keeps the kernel at 96 VGPRs, i.e. 5 waves per SIMD
 // (one register more costs a wave per SIMD and ~10 % on C2); the product instantiations fit without
 // spills, the instrumented (COUNT) ones spill a few registers to scratch.
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) render_kernel(DevScene S, FrameParams F, float* __restrict__ out,
+#ifndef RT_RENDER_WAVES
+#define RT_RENDER_WAVES 5   // variant builds: another waves-per-SIMD target for render_kernel
+#endif
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_RENDER_WAVES))) render_kernel(DevScene S, FrameParams F, float* __restrict__ out,
                                                unsigned long long* __restrict__ counts,
                                                unsigned int* __restrict__ work_counter,
                                                const LaunchConst* __restrict__ lconst) {
