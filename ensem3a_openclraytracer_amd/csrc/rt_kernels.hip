@@ -125,6 +125,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_REN
     int s = 0;
     int cost = 0;   // pass 1: rays this pixel traced (pilot_cost)
     int sun0 = -2;  // the first bounce's shadow-ray hit (-1 = miss; -2 = not traced yet)
+    unsigned long long t_prev = 0;   // COUNT: the wave clock at the previous loop head
 
     // pass 1 (FrameParams::pass): after the pilot samples, save the pixel's state for pass 2; the
     // pixel is written (and its cost set to 0) when all its samples are done
@@ -136,6 +137,13 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_REN
     };
 
     while (true) {
+        // instrumented build: wave cycles in the trace (cyc_trav) and in the rest of the loop (cyc_shade:
+        // every iteration's time, the trace's subtracted below; unsigned wrap-around cancels)
+        if (COUNT && lane == 0) {
+            const unsigned long long now = clock64();
+            if (t_prev) c.cyc_shade += now - t_prev;
+            t_prev = now;
+        }
         // -- refill: ballot the lanes that need a pixel, one atomic per wave --
         // teams (BRUTE, F.team lanes per pixel): one bit per team, the team's lanes take the same pixel
         const unsigned long long need = __ballot(phase == FETCH) & team_leaders;
@@ -259,7 +267,13 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_REN
         // -- one ray per busy lane --
         const rtm_f3 to = (phase == PRIMARY) ? C.position : Bo;
         const rtm_f3 td = (phase == PRIMARY) ? cd : ((phase == BOUNCE) ? Bd : C.sun);
+        const unsigned long long t_tr = COUNT ? clock64() : 0;
         const Hit h = trace<TRAV, COUNT, SMEM, OVF, BRUTE != 0>(S, nodes, tris, to, td, stk, B, lst, c, mtrec, ts, boxrec);
+        if (COUNT && lane == __ffsll((long long)__ballot(1)) - 1) {   // the first tracing lane, once per wave
+            const unsigned long long dt = clock64() - t_tr;
+            c.cyc_trav += dt;
+            c.cyc_shade -= dt;
+        }
         ++cost;
         bool finish = false;
         if (phase == PRIMARY) {
