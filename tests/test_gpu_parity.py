@@ -1439,3 +1439,81 @@ def test_block_handout_renders_identically(kl, case):
         kl.native.set_option("handout", -1)
     with pytest.raises(_native.NativeError, match="handout"):
         kl.native.set_option("handout", 2)
+
+
+# Random triangle soups (seeded): every material type, degenerate (zero-area, collinear), huge and overlapping
+# shifted copies of triangles, coplanar overlaps, coordinates on a 1/64 grid (shared box faces, distance ties;
+# no two centroids equal: the reference BVH.py recurses forever on those).  Scenes of 64 triangles or fewer take the
+# brute-force path, larger ones the tree walk (BVH2, and the 4-wide layout forced).  REF must be bit-identical
+# to the CPU oracle everywhere; every FAST path must equal the others bit for bit (they accept the same
+# triangles by construction) and pass the gate against the oracle.
+RANDOM_SCENES = [(0, 7), (1, 40), (2, 64), (3, 150), (4, 400), (5, 1000), (6, 1), (7, 2), (8, 65), (9, 33),
+                 (10, 300), (11, 2000), (12, 12), (13, 90), (14, 700), (15, 48)]
+
+
+def _random_scene(seed, ntri):
+    import types
+    from ensem3a_openclraytracer_amd import bvh as B
+    rng = np.random.default_rng(1000 + seed)
+    # odd seeds: the soup around the camera (0, -3.5, 0), so camera rays start inside boxes and between triangles
+    c = rng.uniform(-1.5, 1.5, (ntri, 1, 3)) + np.array([0.0, -3.5 if seed % 2 else 1.0, 0.0])
+    tri = c + rng.normal(0.0, 0.35, (ntri, 3, 3)) * rng.choice([0.05, 0.4, 1.0], (ntri, 1, 1))
+    k = max(1, ntri // 10)
+    tri[:k, 2] = tri[:k, 1]                                                        # zero-area (two equal corners)
+    tri[k:2 * k, 2] = 0.5 * (tri[k:2 * k, 0] + tri[k:2 * k, 1])                     # collinear
+    tri[2 * k:3 * k] = tri[3 * k:4 * k] + np.array([1.0 / 64, 0.0, 0.0])              # overlapping shifted copies
+    if ntri >= 8:
+        tri[4 * k:4 * k + 1] *= 8.0                                                # a huge one
+    tri[5 * k:6 * k, :, 2] = np.round(tri[5 * k:6 * k, :, 2])                       # coplanar on z = integer
+    tri = np.round(tri.astype(np.float32) * 64) / 64                               # shared coordinates: ties
+    vp = tri.reshape(-1, 3).astype(np.float32)
+    nrm = rng.normal(size=(ntri, 3)).astype(np.float32)
+    nrm /= np.linalg.norm(nrm, axis=1, keepdims=True)
+    vn = nrm.astype(np.float32)
+    nmat = 5
+    mat = np.array([[1, 0.8, 0.7, 0.6, 0.0, 1.0],      # diffuse
+                    [2, 0.9, 0.9, 0.9, 0.25, 1.0],     # glossy
+                    [3, 0.95, 1.0, 1.0, 0.0, 1.5],     # glass
+                    [0, 1.0, 1.0, 1.0, 3.0, 1.0],      # emitter (emission = roughness)
+                    [1, 0.2, 0.5, 0.9, 0.0, 1.0]], np.float32)
+    face = np.zeros((ntri, 10), np.int32)
+    face[:, 0] = rng.integers(0, nmat, ntri)
+    face[:, 4:7] = np.arange(ntri)[:, None]
+    face[:, 7:10] = np.arange(3 * ntri).reshape(ntri, 3)
+    fd = face.ravel()
+    return types.SimpleNamespace(V_p=vp.ravel(), V_n=vn.ravel(), V_uv=np.zeros(2, np.float32), faceData=fd,
+                                 materialData=mat.ravel(), lightData=np.zeros(0, np.float32), BVH=B.BVH(fd, vp.ravel()))
+
+
+@pytest.mark.parametrize("seed,ntri", RANDOM_SCENES)
+def test_random_scenes_match_oracle(kl, seed, ntri):
+    import json
+    sc = _random_scene(seed, ntri)
+    _, cam, env, _, _, _, ibl = W.PARITY_CASES["serre_96x54_s4"].inputs()   # a lit IBL and sun
+    cam = np.array(W.PARITY_CASES["cornell_64_s4"].inputs()[1], np.float32).copy()
+    cam[6] = 40.0
+    npix, spp, mb = 40 * 40, 4, 4
+    ora = _oracle(sc, cam, env, npix, spp, mb, ibl)
+    ref = _launch(kl, sc, cam, env, npix, spp, mb, ibl, "ref")
+    np.testing.assert_array_equal(ref, ora)
+    fast = _launch(kl, sc, cam, env, npix, spp, mb, ibl, "fast")
+    st = compare.assert_gate(fast, ora, f"random scene {seed} ({ntri} triangles) FAST vs oracle")
+    others = {}
+    try:
+        if ntri <= 64:
+            kl.native.set_option("brute_max", 0)        # the tree walk instead of the brute force
+            others["tree"] = _launch(kl, sc, cam, env, npix, spp, mb, ibl, "fast")
+            kl.native.set_option("brute_max", 64)
+        else:
+            kl.native.set_option("bvh_width", 4)        # the 4-wide quantised layout
+            others["wide"] = _launch(kl, sc, cam, env, npix, spp, mb, ibl, "fast")
+            kl.native.set_option("bvh_width", 0)
+    finally:
+        kl.native.set_option("brute_max", 64)
+        kl.native.set_option("bvh_width", 0)
+    for name, f in others.items():
+        np.testing.assert_array_equal(f, fast, err_msg=name)
+    diff = int(np.unique(np.nonzero(fast != ora)[0] // 3).size)
+    print(json.dumps({"seed": seed, "tris": ntri, "fast_non_identical": diff, "frac_identical": st["frac_identical"],
+                      "checked": ["ref==oracle"] + [f"fast=={k}" for k in others]}))
+    assert diff <= npix // 100, diff
