@@ -1489,10 +1489,15 @@ def _random_scene(seed, ntri):
 def test_random_scenes_match_oracle(kl, seed, ntri):
     import json
     sc = _random_scene(seed, ntri)
-    _, cam, env, _, _, _, ibl = W.PARITY_CASES["serre_96x54_s4"].inputs()   # a lit IBL and sun
-    cam = np.array(W.PARITY_CASES["cornell_64_s4"].inputs()[1], np.float32).copy()
-    cam[6] = 40.0
-    npix, spp, mb = 40 * 40, 4, 4
+    ibl = W.ibl_preview()
+    rng = np.random.default_rng(7000 + seed)
+    # camera at (0, -3.5, 0), rotated a little, a random field of view; sun direction, sun and IBL power and
+    # bounce count vary per seed (IBL power 0 / sun power 0 included: the shortcuts that skip them)
+    cam = np.array([0.0, -3.5, 0.0, *rng.uniform(-12.0, 12.0, 3), 40, 40, 1,
+                    float(rng.choice([30.0, 45.0, 75.0])) * (3.14 / 180)], np.float64).astype(np.float32)
+    env = np.array([*rng.uniform(-180.0, 180.0, 3), rng.choice([0.0, 0.5, 2.0]), rng.choice([0.0, 0.3, 1.0])],
+                   np.float64).astype(np.float32)
+    npix, spp, mb = 40 * 40, 4, int(rng.choice([0, 1, 2, 4, 7]))
     ora = _oracle(sc, cam, env, npix, spp, mb, ibl)
     ref = _launch(kl, sc, cam, env, npix, spp, mb, ibl, "ref")
     np.testing.assert_array_equal(ref, ora)
@@ -1514,6 +1519,7 @@ def test_random_scenes_match_oracle(kl, seed, ntri):
     for name, f in others.items():
         np.testing.assert_array_equal(f, fast, err_msg=name)
     diff = int(np.unique(np.nonzero(fast != ora)[0] // 3).size)
-    print(json.dumps({"seed": seed, "tris": ntri, "fast_non_identical": diff, "frac_identical": st["frac_identical"],
+    print(json.dumps({"seed": seed, "tris": ntri, "max_bounce": mb, "env": [round(float(x), 2) for x in env],
+                      "fast_non_identical": diff, "frac_identical": st["frac_identical"],
                       "checked": ["ref==oracle"] + [f"fast=={k}" for k in others]}))
     assert diff <= npix // 100, diff
